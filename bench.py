@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py -- SHA-256 nonce-search throughput (BASELINE.json metric: GH/s at
+1/2/4/8 MI355X and % of the VALU integer roofline).
+
+One step = one search (the miner's scan over bitcoin.Hash, reference
+bitcoin/hash.go:13-17 + miner spec SURVEY.md §8(a) A2) of a 2^32-nonce shard of
+msg "cmu440" per GPU -- BASELINE.json configs[1] (single SHA block, nonces
+0..2^32-1 spanning every decimal-length bucket d = 1..10) at N = 1 -- followed by
+the 16-byte (hash, nonce) merge across ranks.  Weak scaling: rank r scans
+[r*2^32, (r+1)*2^32 - 1]; the only exchange is the 16-byte tuple per rank.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+Rank 0 prints ONE JSON line.  `roofline` comes from HIP events the library
+records around every fast-kernel launch on its own stream during the timed
+region (mh_profile_*); `cpu_baseline` times the CPU port of the reference loop
+(oracle/) on a bounded sample, at N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "bitcoin-miner_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of VALU int roofline"
+PEAK_SCLK_HZ = 2.4e9          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
+LANES_PER_CU_CLK = 4 * 32     # 4 SIMD-32 per CU: a wave64 VALU op issues in 2 cycles
+OPS_PER_BLOCK = 1376          # canonical gfx950 VALU ops per SHA-256 compression
+
+
+def shard(rank, bits):
+    lo = rank << bits
+    return lo, lo + (1 << bits) - 1
+
+
+def merge(results):
+    """Lexicographic (hash, nonce) minimum == the reference loop's strict-< first min."""
+    return min(results)
+
+
+def gather_merge(r, world, dist, torch, device):
+    if world == 1:
+        return r
+    import numpy as np
+    t = torch.from_numpy(np.array([r[0], r[1]], dtype=np.uint64).view(np.int64)).to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    vals = [tuple(int(v) for v in o.cpu().numpy().view(np.uint64)) for o in out]
+    return merge(vals)
+
+
+def run_steps(search, lo, hi, steps, warmup, world, dist, torch, device, sync):
+    """Warmup, then exactly `steps` timed searches + merges between barriers.
+    Returns (merged result, this rank's elapsed seconds)."""
+    r = None
+    for _ in range(warmup):
+        r = gather_merge(search(lo, hi), world, dist, torch, device)
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r = gather_merge(search(lo, hi), world, dist, torch, device)
+    if world > 1:
+        dist.barrier()
+    sync()
+    return r, time.perf_counter() - t0
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(msg, threads):
+    """The reference loop ported to C (oracle/): per nonce format "%s %d" and a
+    full SHA-256 from the IV, like bitcoin/hash.go.  Bounded sample of the
+    same workload (d = 10 nonces, the bulk of configs[1])."""
+    from oracle import oracle
+    base = 10 ** 9
+    n1 = 6_000_000
+    t = time.perf_counter()
+    oracle.search(msg, base, base + n1 - 1, threads=1)
+    st = n1 / (time.perf_counter() - t)
+    nT = 12_000_000 * threads
+    t = time.perf_counter()
+    oracle.search(msg, base, base + nT - 1, threads=threads)
+    mt = nT / (time.perf_counter() - t)
+    return {
+        "value": mt / 1e9, "unit": "GH/s", "cores": threads, "kind": "port",
+        "sample": f"msg {msg!r}, nonces [1e9, 1e9+{nT}) on {threads} threads "
+                  f"({cpu_model()}); single thread {n1} nonces: {st / 1e6:.3f} MH/s",
+        "single_thread_value": st / 1e9,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--msg", default="cmu440")
+    ap.add_argument("--bits", type=int, default=32, help="log2 nonces per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    import torch
+    dist = None
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    import minehip
+    if minehip.device_count() <= local:
+        raise RuntimeError(f"rank {rank}: no HIP device {local}")
+    msg = args.msg.encode()
+    lo, hi = shard(rank, args.bits)
+
+    def search(a, b):
+        return minehip.search(msg, a, b, local)
+
+    for _ in range(args.warmup):
+        search(lo, hi)
+    minehip.profile_enable(local, True)
+    r, elapsed = run_steps(search, lo, hi, args.steps, 0, world, dist, torch, device, torch.cuda.synchronize)
+    prof = minehip.profile_read(local)
+    minehip.profile_enable(local, False)
+
+    t_max = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+
+    nonces = world * (1 << args.bits) * args.steps
+    value = nonces / t_max / 1e9
+    props = torch.cuda.get_device_properties(device)
+    cus = int(props.multi_processor_count)
+    peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
+    achieved = prof["fast_ops"] / (prof["fast_ns"] * 1e-9) / 1e12 if prof["fast_ns"] else 0.0
+    launches = max(1, prof["fast_launches"])
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(args.msg, threads)
+        from oracle import oracle
+        line = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "GH/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"BASELINE configs[1]: msg {args.msg!r}, 2^{args.bits} nonces per GPU "
+                            f"(rank r scans [r*2^{args.bits}, (r+1)*2^{args.bits}-1]), single SHA block",
+                "msg": args.msg, "nonces_per_gpu": 1 << args.bits, "parallelism": f"shard x{world}",
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved, 3),
+                "peak": round(peak, 3),
+                "unit": "TOPS (int32 VALU)",
+                "frac": round(achieved / peak, 4) if peak else None,
+                "traffic": None,
+                "kernel": "fast_search",
+                "ops_per_nonce": OPS_PER_BLOCK,
+                "avg_launch_ms": round(prof["fast_ns"] / launches / 1e6, 4),
+                "launches": prof["fast_launches"],
+                "kernel_ghs": round(prof["fast_nonces"] / (prof["fast_ns"] * 1e-9) / 1e9, 4)
+                if prof["fast_ns"] else None,
+                "peak_basis": f"{cus} CU x {LANES_PER_CU_CLK} lanes/clk x {PEAK_SCLK_HZ / 1e9} GHz",
+            },
+            "cpu_baseline": cpu,
+            "result": {"hash": r[0], "nonce": r[1],
+                       "rehash_ok": oracle.hash_(msg, r[1]) == r[0]},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+// layout.hpp -- host/device shared launch descriptors for libminehip.
+//
+// The message the reference hashes per nonce is  msg ' ' decimal(nonce)
+// (bitcoin/hash.go:15).  The host absorbs every full 64-byte block of the
+// constant prefix P = msg ' ' into a midstate; what remains is the "tail":
+// t = len(P) mod 64 prefix bytes, then the d digits, 0x80, zeros and the
+// 64-bit bit length -- one or two 64-byte tail blocks (tail byte positions
+// 0..127, big-endian words 0..31).
+//
+// A search over one decimal-length bucket (all nonces have d digits) splits
+// every nonce n = U * 10^L + q into a run index U (the d-L "higher" digits,
+// one run per GPU lane) and q in [0, 10^L) (the L "lower" digits, enumerated
+// inside the lane).  See DESIGN.md §3.
+#pragma once
+#include <stdint.h>
+
+namespace mh {
+
+constexpr int kBlockThreads = 256;         // 4 waves of 64 per workgroup
+constexpr uint32_t kMaxBlocksPerLaunch = 65536;
+
+struct Partial {          // one (hash, nonce) candidate; ordered lexicographically
+    uint64_t hash;
+    uint64_t nonce;
+};
+
+enum FastMode : uint32_t {
+    kModeOne = 0,   // one tail block, compressed per nonce from the host midstate
+    kModePre = 1,   // two tail blocks; block 0 holds no lower digit and is compressed once per run
+    kModeTwo = 2,   // two tail blocks; the lower digits sit in block 0 -> both blocks per nonce
+};
+
+// Arguments of the fast (run) kernel.  Passed by value: lands in SGPRs.
+struct FastArgs {
+    uint32_t mid[8];      // chaining state before tail block 0
+    uint32_t blk[32];     // tail words: prefix bytes, '0' at every digit byte, 0x80, bit length
+    uint64_t u_start;     // run index U of lane 0 of block 0
+    uint64_t pow10L;      // 10^L
+    uint32_t n_runs;      // active lanes in this launch
+    uint32_t hi_end;      // tail byte index one past U's last digit
+    uint32_t n_hi;        // digits of U (= d - L)
+    uint32_t lo_pos;      // byte index (within the per-nonce block) of the first lower digit
+    uint32_t L;           // lower digits enumerated inside a lane (1..5)
+    uint32_t n_groups;    // 10^(L-1): groups of 10 consecutive nonces per lane
+    uint32_t mode;        // FastMode
+    uint32_t pad;
+    uint32_t kw1[64];     // kModeTwo: K[i] + W[i] of tail block 1 (padding + length only)
+};
+
+// Arguments of the generic per-nonce kernels (range edges, small buckets,
+// batch hashing): any nonce, any digit count, one nonce per lane.
+struct GenArgs {
+    uint32_t mid[8];      // chaining state before tail block 0
+    uint32_t tail[16];    // the t prefix bytes of the tail, zero elsewhere
+    uint64_t plen;        // len(msg) + 1 (bytes before the digits, all blocks)
+    uint64_t first;       // scan: first nonce
+    uint64_t count;       // scan: nonces in this launch
+    uint32_t t;           // tail prefix length, 0..63
+    uint32_t pad;
+};
+
+}  // namespace mh

@@ -1,0 +1,412 @@
+// minehip.cpp -- C-ABI of libminehip.so (declared in include/minehip.h).
+//
+// Per device: one HIP stream, a partials buffer, a 16-byte running minimum
+// and a pinned 16-byte host slot, created on first use and reused by every
+// call.  A search enqueues all of its launches (fast runs, generic edges,
+// merges) on that stream and synchronises once, when it copies the 16-byte
+// result back.  No CPU fallback exists: without a gfx950 device the calls fail
+// with MH_ENODEV.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/minehip.h"
+#include "layout.hpp"
+#include "plan.hpp"
+
+namespace mh {
+hipError_t launch_fast(int J, bool two, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
+hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
+hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
+                             hipStream_t s);
+hipError_t launch_merge(const Partial* partials, uint32_t n, Partial* best, hipStream_t s);
+}  // namespace mh
+
+namespace {
+
+using mh::Partial;
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& what) {
+    g_err = what;
+    return code;
+}
+
+}  // namespace
+
+namespace mh {
+int set_error(int code, const char* what) { return fail(code, what); }
+}  // namespace mh
+
+namespace {
+
+#define MH_HIP(call)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (call);                                                                      \
+        if (e_ != hipSuccess) return fail(MH_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr uint64_t kBatchChunk = 1u << 22;  // nonces per hash_batch transfer
+constexpr int kEventPairs = 512;             // profiled launches buffered before harvesting
+
+struct Timed {
+    hipEvent_t start, stop;
+    int kind;  // 0 fast, 1 generic
+};
+
+struct DevCtx {
+    std::mutex mu;
+    int dev = -1;
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    Partial* d_partials = nullptr;
+    Partial* d_best = nullptr;
+    Partial* h_best = nullptr;  // pinned
+    uint64_t* d_nonces = nullptr;
+    uint64_t* d_hashes = nullptr;
+    // profiling
+    bool prof = false;
+    std::vector<Timed> pool;
+    int used = 0;
+    uint64_t cnt[8] = {0};
+};
+
+std::mutex g_tab_mu;
+std::vector<std::unique_ptr<DevCtx>> g_tab;
+int g_ndev = -1;
+
+int device_count_impl() {
+    std::lock_guard<std::mutex> lk(g_tab_mu);
+    if (g_ndev < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_ndev = n;
+        g_tab.resize((size_t)n);
+        for (auto& p : g_tab) p.reset(new DevCtx());
+    }
+    return g_ndev;
+}
+
+// Returns the context for dev, initialised, with its mutex NOT held.
+int get_ctx(int dev, DevCtx** out) {
+    const int n = device_count_impl();
+    if (n <= 0) return fail(MH_ENODEV, "no HIP device visible");
+    if (dev < 0 || dev >= n) return fail(MH_EINVAL, "device index out of range");
+    DevCtx* c = g_tab[(size_t)dev].get();
+    *out = c;
+    return MH_OK;
+}
+
+int init_locked(DevCtx* c, int dev) {
+    if (c->ready) return MH_OK;
+    MH_HIP(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    MH_HIP(hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(MH_ENODEV, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950 only");
+    MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
+    MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
+    MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
+    MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
+    MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
+    c->pool.resize(kEventPairs);
+    for (auto& t : c->pool) {
+        MH_HIP(hipEventCreate(&t.start));
+        MH_HIP(hipEventCreate(&t.stop));
+    }
+    c->dev = dev;
+    c->ready = true;
+    return MH_OK;
+}
+
+// Stream must be idle or synchronised by the caller.
+int harvest_locked(DevCtx* c) {
+    for (int i = 0; i < c->used; ++i) {
+        float ms = 0.f;
+        MH_HIP(hipEventElapsedTime(&ms, c->pool[(size_t)i].start, c->pool[(size_t)i].stop));
+        const uint64_t ns = (uint64_t)((double)ms * 1.0e6);
+        c->cnt[c->pool[(size_t)i].kind == 0 ? 2 : 5] += ns;
+    }
+    c->used = 0;
+    return MH_OK;
+}
+
+// Enqueue one piece (kernel + merge) on the context's stream.
+int enqueue_piece(DevCtx* c, const mh::Piece& p) {
+    Timed* tm = nullptr;
+    if (c->prof) {
+        if (c->used == kEventPairs) {
+            MH_HIP(hipStreamSynchronize(c->stream));
+            int rc = harvest_locked(c);
+            if (rc) return rc;
+        }
+        tm = &c->pool[(size_t)c->used++];
+        tm->kind = p.kind;
+        MH_HIP(hipEventRecord(tm->start, c->stream));
+    }
+    uint32_t blocks;
+    if (p.kind == 0) {
+        // host-side shape checks: the grid covers exactly n_runs lanes and the
+        // partials buffer holds one slot per block
+        if (p.fa.n_runs == 0 || p.fa.L < 1 || p.fa.L > 5 || p.fa.n_hi + p.fa.L > 20)
+            return fail(MH_EINVAL, "internal: bad fast piece");
+        blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
+        if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINVAL, "internal: fast grid too large");
+        MH_HIP(mh::launch_fast(p.J, p.mode == mh::kModeTwo, p.fa, c->d_partials, blocks, c->stream));
+    } else {
+        if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
+            return fail(MH_EINVAL, "internal: bad generic piece");
+        blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
+        MH_HIP(mh::launch_generic_scan(p.ga, c->d_partials, blocks, c->stream));
+    }
+    if (tm) MH_HIP(hipEventRecord(tm->stop, c->stream));
+    MH_HIP(mh::launch_merge(c->d_partials, blocks, c->d_best, c->stream));
+    if (c->prof) {
+        if (p.kind == 0) {
+            c->cnt[0] += 1;
+            c->cnt[1] += p.count;
+            c->cnt[3] += p.count * (uint64_t)p.blocks * (uint64_t)MH_OPS_PER_BLOCK;
+        } else {
+            c->cnt[4] += p.count;
+        }
+    }
+    return MH_OK;
+}
+
+// Planner knobs, overridable for tests and tuning (the result never depends
+// on them -- tests/test_gpu_parity.py checks exactly that):
+//   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 3)
+//   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^32)
+mh::PlanOpts plan_opts() {
+    mh::PlanOpts o;
+    if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 5) o.lower_digits = v;
+    }
+    if (const char* e = getenv("MINEHIP_LAUNCH_NONCES")) {
+        const unsigned long long v = strtoull(e, nullptr, 10);
+        if (v >= 1) o.max_nonces_per_launch = v;
+    }
+    return o;
+}
+
+int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, uint64_t* oh, uint64_t* on) {
+    DevCtx* c;
+    int rc = get_ctx(dev, &c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    rc = init_locked(c, dev);
+    if (rc) return rc;
+    MH_HIP(hipSetDevice(dev));
+    MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
+    const mh::PlanOpts opt = plan_opts();
+    int err = MH_OK;
+    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
+        err = enqueue_piece(c, p);
+        return err == MH_OK;
+    });
+    if (err) {
+        (void)hipStreamSynchronize(c->stream);
+        return err;
+    }
+    MH_HIP(hipMemcpyAsync(c->h_best, c->d_best, sizeof(Partial), hipMemcpyDeviceToHost, c->stream));
+    MH_HIP(hipStreamSynchronize(c->stream));
+    if (c->prof) {
+        rc = harvest_locked(c);
+        if (rc) return rc;
+    }
+    *oh = c->h_best->hash;
+    *on = c->h_best->nonce;
+    return MH_OK;
+}
+
+int check_common(const uint8_t* msg, size_t len) {
+    if (msg == nullptr && len != 0) return fail(MH_EINVAL, "msg is NULL");
+    if (len > MH_MAX_MSG_LEN) return fail(MH_ETOOLONG, "message longer than MH_MAX_MSG_LEN");
+    return MH_OK;
+}
+
+inline bool lex_less(uint64_t ha, uint64_t na, uint64_t hb, uint64_t nb) {
+    return ha < hb || (ha == hb && na < nb);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mh_abi_version(void) { return MH_ABI_VERSION; }
+
+int mh_device_count(void) { return device_count_impl(); }
+
+const char* mh_last_error(void) { return g_err.c_str(); }
+
+int mh_search(int dev, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, uint64_t* out_hash,
+              uint64_t* out_nonce) {
+    g_err.clear();
+    if (!out_hash || !out_nonce) return fail(MH_EINVAL, "NULL output pointer");
+    int rc = check_common(msg, len);
+    if (rc) return rc;
+    if (lower > upper) return fail(MH_ERANGE, "lower > upper");
+    mh::Prefix pre;
+    mh::absorb_prefix(msg, len, &pre);
+    return search_impl(dev, pre, lower, upper, out_hash, out_nonce);
+}
+
+int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper,
+                    uint64_t chunk, uint64_t* out_hash, uint64_t* out_nonce) {
+    g_err.clear();
+    if (!out_hash || !out_nonce || !devs || ndev <= 0) return fail(MH_EINVAL, "bad arguments");
+    int rc = check_common(msg, len);
+    if (rc) return rc;
+    if (lower > upper) return fail(MH_ERANGE, "lower > upper");
+    const int n = mh_device_count();
+    for (int i = 0; i < ndev; ++i)
+        if (devs[i] < 0 || devs[i] >= n) return fail(n <= 0 ? MH_ENODEV : MH_EINVAL, "device index out of range");
+    mh::Prefix pre;
+    mh::absorb_prefix(msg, len, &pre);
+    const uint64_t span = upper - lower;  // count - 1
+    if (chunk == 0) {
+        // >= 8 chunks per device for dynamic balance, >= 2^32 nonces each
+        const uint64_t want = span / ((uint64_t)ndev * 8u) + 1u;
+        chunk = want < (1ull << 32) ? (1ull << 32) : want;
+    }
+    const uint64_t nchunks = span / chunk + 1u;  // chunk >= 1
+    std::atomic<uint64_t> next{0};
+    std::atomic<int> first_err{0};
+    std::vector<Partial> best((size_t)ndev, Partial{~0ull, ~0ull});
+    std::vector<std::string> errs((size_t)ndev);
+    std::vector<std::thread> th;
+    for (int i = 0; i < ndev; ++i) {
+        th.emplace_back([&, i]() {
+            for (;;) {
+                if (first_err.load() != 0) return;
+                const uint64_t k = next.fetch_add(1);
+                if (k >= nchunks) return;
+                const uint64_t a = lower + k * chunk;
+                const uint64_t b = (upper - a < chunk - 1u) ? upper : a + (chunk - 1u);
+                uint64_t h, nn;
+                const int r = search_impl(devs[i], pre, a, b, &h, &nn);
+                if (r) {
+                    errs[(size_t)i] = g_err;
+                    int z = 0;
+                    first_err.compare_exchange_strong(z, r);
+                    return;
+                }
+                if (lex_less(h, nn, best[(size_t)i].hash, best[(size_t)i].nonce)) best[(size_t)i] = Partial{h, nn};
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    if (first_err.load()) {
+        for (auto& e : errs)
+            if (!e.empty()) return fail(first_err.load(), e);
+        return fail(first_err.load(), "device worker failed");
+    }
+    Partial r = best[0];
+    for (int i = 1; i < ndev; ++i)
+        if (lex_less(best[(size_t)i].hash, best[(size_t)i].nonce, r.hash, r.nonce)) r = best[(size_t)i];
+    *out_hash = r.hash;
+    *out_nonce = r.nonce;
+    return MH_OK;
+}
+
+int mh_hash_batch(int dev, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n, uint64_t* out_hashes) {
+    g_err.clear();
+    int rc = check_common(msg, len);
+    if (rc) return rc;
+    if (n == 0) return MH_OK;
+    if (!nonces || !out_hashes) return fail(MH_EINVAL, "NULL buffer");
+    DevCtx* c;
+    rc = get_ctx(dev, &c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    rc = init_locked(c, dev);
+    if (rc) return rc;
+    MH_HIP(hipSetDevice(dev));
+    mh::Prefix pre;
+    mh::absorb_prefix(msg, len, &pre);
+    mh::GenArgs ga;
+    mh::make_gen_args(pre, &ga);
+    for (size_t off = 0; off < n; off += kBatchChunk) {
+        const size_t m = (n - off < kBatchChunk) ? n - off : kBatchChunk;
+        MH_HIP(hipMemcpyAsync(c->d_nonces, nonces + off, m * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        MH_HIP(mh::launch_hash_batch(ga, c->d_nonces, c->d_hashes, m, c->stream));
+        MH_HIP(hipMemcpyAsync(out_hashes + off, c->d_hashes, m * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        MH_HIP(hipStreamSynchronize(c->stream));
+    }
+    return MH_OK;
+}
+
+int mh_profile_enable(int dev, int on) {
+    g_err.clear();
+    DevCtx* c;
+    int rc = get_ctx(dev, &c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    rc = init_locked(c, dev);
+    if (rc) return rc;
+    MH_HIP(hipStreamSynchronize(c->stream));
+    c->used = 0;
+    memset(c->cnt, 0, sizeof c->cnt);
+    c->prof = on != 0;
+    return MH_OK;
+}
+
+int mh_profile_read(int dev, uint64_t* out, int n) {
+    g_err.clear();
+    if (!out || n < 0) return fail(MH_EINVAL, "bad arguments");
+    DevCtx* c;
+    int rc = get_ctx(dev, &c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->ready) {
+        MH_HIP(hipStreamSynchronize(c->stream));
+        rc = harvest_locked(c);
+        if (rc) return rc;
+    }
+    for (int i = 0; i < n && i < 8; ++i) out[i] = c->cnt[i];
+    return MH_OK;
+}
+
+int64_t mh_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, mh_piece* out, int64_t cap) {
+    g_err.clear();
+    int rc = check_common(msg, len);
+    if (rc) return rc;
+    if (lower > upper) return fail(MH_ERANGE, "lower > upper");
+    if (cap < 0) return fail(MH_EINVAL, "cap < 0");
+    mh::Prefix pre;
+    mh::absorb_prefix(msg, len, &pre);
+    int64_t k = 0;
+    const mh::PlanOpts opt = plan_opts();
+    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
+        if (k >= cap) {
+            ++k;  // cap + 1 signals truncation
+            return false;
+        }
+        if (out) {
+            mh_piece& q = out[k];
+            q.first = p.first;
+            q.count = p.count;
+            q.kind = p.kind;
+            q.digits = p.digits;
+            q.lo_digits = p.L;
+            q.word = p.J;
+            q.mode = p.mode;
+            q.blocks = p.blocks;
+        }
+        ++k;
+        return true;
+    });
+    return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,244 @@
+// plan.cpp -- see plan.hpp.
+#include "plan.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+
+namespace mh {
+namespace {
+
+constexpr uint32_t kK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+constexpr uint32_t kIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                             0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+inline uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+constexpr uint64_t kPow10[20] = {1ull,
+                                 10ull,
+                                 100ull,
+                                 1000ull,
+                                 10000ull,
+                                 100000ull,
+                                 1000000ull,
+                                 10000000ull,
+                                 100000000ull,
+                                 1000000000ull,
+                                 10000000000ull,
+                                 100000000000ull,
+                                 1000000000000ull,
+                                 10000000000000ull,
+                                 100000000000000ull,
+                                 1000000000000000ull,
+                                 10000000000000000ull,
+                                 100000000000000000ull,
+                                 1000000000000000000ull,
+                                 10000000000000000000ull};
+
+// big-endian byte i of a 32-word tail image
+inline void put_byte(uint32_t* w, uint32_t pos, uint32_t v) { w[pos >> 2] |= v << (24u - 8u * (pos & 3u)); }
+
+void schedule(const uint32_t w16[16], uint32_t w[64]) {
+    for (int i = 0; i < 16; ++i) w[i] = w16[i];
+    for (int i = 16; i < 64; ++i) {
+        const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+}
+
+}  // namespace
+
+int decimal_digits(uint64_t n) {
+    int d = 1;
+    while (d < 20 && n >= kPow10[d]) ++d;
+    return d;
+}
+
+void host_compress(uint32_t st[8], const uint32_t w16[16]) {
+    uint32_t w[64];
+    schedule(w16, w);
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t t1 = h + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + kK[i] + w[i];
+        const uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+void absorb_prefix(const uint8_t* msg, size_t len, Prefix* out) {
+    memcpy(out->mid, kIV, sizeof kIV);
+    out->plen = (uint64_t)len + 1u;
+    const uint64_t nfull = out->plen / 64u;
+    uint32_t w[16];
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+        for (int i = 0; i < 16; ++i) {
+            uint32_t v = 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t p = blk * 64u + (uint64_t)(4 * i + k);
+                const uint32_t byte = (p < len) ? msg[p] : (uint32_t)' ';
+                v = (v << 8) | byte;
+            }
+            w[i] = v;
+        }
+        host_compress(out->mid, w);
+    }
+    out->t = (uint32_t)(out->plen % 64u);
+    memset(out->tail, 0, sizeof out->tail);
+    for (uint32_t i = 0; i < out->t; ++i) {
+        const uint64_t p = nfull * 64u + i;
+        out->tail[i] = (p < len) ? msg[p] : (uint8_t)' ';
+    }
+}
+
+void make_gen_args(const Prefix& pre, GenArgs* ga) {
+    memset(ga, 0, sizeof *ga);
+    memcpy(ga->mid, pre.mid, sizeof pre.mid);
+    for (uint32_t i = 0; i < pre.t; ++i) put_byte(ga->tail, i, pre.tail[i]);
+    ga->plen = pre.plen;
+    ga->t = pre.t;
+}
+
+namespace {
+
+// Fast-kernel launch template for bucket d with L lower digits.
+bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, int* blocks_out, FastArgs* fa) {
+    const uint32_t t = pre.t;
+    const uint32_t total = t + (uint32_t)d;
+    const int nb = (total + 9u <= 64u) ? 1 : 2;
+    const uint32_t pl = total - 1u;  // tail byte of the last digit
+    int mode;
+    uint32_t base;
+    if (nb == 1) {
+        mode = kModeOne;
+        base = 0;
+    } else if (pl >= 64u) {
+        mode = kModePre;
+        base = 64;
+        if (pl - (uint32_t)L + 1u < 64u) return false;  // every lower digit must sit in block 1
+    } else {
+        mode = kModeTwo;
+        base = 0;
+    }
+    const uint32_t lo = pl - (uint32_t)L + 1u - base;  // first lower digit, per-nonce-block relative
+    const int J = (int)((pl - base) >> 2);
+    if ((int)(lo >> 2) < J - 1) return false;  // lower digits must span words J-1..J only
+    if (mode == kModeTwo ? (J < 13 || J > 15) : (J < 0 || J > 13)) return false;
+
+    memset(fa, 0, sizeof *fa);
+    memcpy(fa->mid, pre.mid, sizeof pre.mid);
+    for (uint32_t i = 0; i < t; ++i) put_byte(fa->blk, i, pre.tail[i]);
+    for (uint32_t i = 0; i < (uint32_t)d; ++i) put_byte(fa->blk, t + i, 0x30u);  // '0' in every digit byte
+    put_byte(fa->blk, total, 0x80u);
+    const uint64_t bits = (pre.plen + (uint64_t)d) * 8u;
+    const int lw = nb * 16 - 2;
+    fa->blk[lw] = (uint32_t)(bits >> 32);
+    fa->blk[lw + 1] = (uint32_t)bits;
+    fa->pow10L = kPow10[L];
+    fa->hi_end = total - (uint32_t)L;
+    fa->n_hi = (uint32_t)(d - L);
+    fa->lo_pos = lo;
+    fa->L = (uint32_t)L;
+    fa->n_groups = (uint32_t)kPow10[L - 1];
+    fa->mode = (uint32_t)mode;
+    if (mode == kModeTwo) {
+        uint32_t w[64];
+        schedule(fa->blk + 16, w);
+        for (int i = 0; i < 64; ++i) fa->kw1[i] = kK[i] + w[i];
+    }
+    *J_out = J;
+    *mode_out = mode;
+    *blocks_out = nb;
+    return true;
+}
+
+}  // namespace
+
+void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
+                 const std::function<bool(const Piece&)>& cb) {
+    GenArgs gbase;
+    make_gen_args(pre, &gbase);
+    const int d_lo = decimal_digits(lower), d_hi = decimal_digits(upper);
+    const uint64_t max_gen = (uint64_t)kMaxBlocksPerLaunch * kBlockThreads;
+
+    auto emit_generic = [&](uint64_t a, uint64_t b, int d) -> bool {  // [a, b] inclusive, a <= b
+        for (;;) {
+            const uint64_t left = b - a;  // count - 1
+            const uint64_t cnt = (left >= max_gen - 1u) ? max_gen : left + 1u;
+            Piece p;
+            memset(&p, 0, sizeof p);
+            p.first = a;
+            p.count = cnt;
+            p.kind = 1;
+            p.digits = d;
+            p.blocks = ((pre.t + (uint32_t)d + 9u) <= 64u) ? 1 : 2;
+            p.ga = gbase;
+            p.ga.first = a;
+            p.ga.count = cnt;
+            if (!cb(p)) return false;
+            if (cnt - 1u == left) return true;
+            a += cnt;
+        }
+    };
+
+    for (int d = d_lo; d <= d_hi; ++d) {
+        const uint64_t A = std::max<uint64_t>(lower, d == 1 ? 0u : kPow10[d - 1]);
+        const uint64_t B = std::min<uint64_t>(upper, d == 20 ? ~(uint64_t)0 : kPow10[d] - 1u);
+        int L = std::min(opt.lower_digits, d - 1);
+        L = std::min(L, 5);
+        FastArgs fa;
+        int J = 0, mode = 0, nb = 1;
+        while (L >= 1 && !make_fast_args(pre, d, L, &J, &mode, &nb, &fa)) --L;
+        if (L < 1) {
+            if (!emit_generic(A, B, d)) return;
+            continue;
+        }
+        const unsigned __int128 R = kPow10[L];
+        const unsigned __int128 U0 = ((unsigned __int128)A + R - 1u) / R;
+        const unsigned __int128 U1p = ((unsigned __int128)B + 1u) / R;  // one past the last full run
+        if (U0 >= U1p) {
+            if (!emit_generic(A, B, d)) return;
+            continue;
+        }
+        const uint64_t fast_first = (uint64_t)(U0 * R);
+        const unsigned __int128 fast_end = U1p * R;  // exclusive, may be 2^64
+        if (A < fast_first && !emit_generic(A, fast_first - 1u, d)) return;
+        const uint64_t max_runs =
+            std::max<uint64_t>(1u, std::min<uint64_t>((uint64_t)kMaxBlocksPerLaunch * kBlockThreads,
+                                                      opt.max_nonces_per_launch / (uint64_t)R));
+        for (unsigned __int128 u = U0; u < U1p;) {
+            const unsigned __int128 left = U1p - u;
+            const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
+            Piece p;
+            memset(&p, 0, sizeof p);
+            p.first = (uint64_t)(u * R);
+            p.count = (uint64_t)((unsigned __int128)runs * R);
+            p.kind = 0;
+            p.digits = d;
+            p.L = L;
+            p.J = J;
+            p.mode = mode;
+            p.blocks = nb;
+            p.fa = fa;
+            p.fa.u_start = (uint64_t)u;
+            p.fa.n_runs = (uint32_t)runs;
+            p.ga = gbase;
+            if (!cb(p)) return;
+            u += runs;
+        }
+        if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
+    }
+}
+
+}  // namespace mh

@@ -1,0 +1,62 @@
+// plan.hpp -- host-side search planning for libminehip (no HIP dependency).
+//
+// Splits a Request range [lower, upper] (bitcoin/message.go:18-34) into
+// kernel launches: per decimal-length bucket, the nonces that form whole runs
+// of 10^L go to fast_search, the ragged edges and tiny buckets go to
+// generic_scan.  The prefix "msg " is absorbed here into a SHA-256 midstate
+// (the constant part of fmt.Sprintf("%s %d") at bitcoin/hash.go:15).
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#include <functional>
+
+#include "layout.hpp"
+
+namespace mh {
+
+// Every full 64-byte block of P = msg ' ' compressed into mid; the rest of P
+// is the tail.
+struct Prefix {
+    uint32_t mid[8];
+    uint8_t tail[64];
+    uint32_t t;     // len(P) mod 64
+    uint64_t plen;  // len(P) = len(msg) + 1
+};
+
+void absorb_prefix(const uint8_t* msg, size_t len, Prefix* out);
+
+// FIPS 180-4 compression on the host (midstates and the fixed schedule of a
+// padding-only block).
+void host_compress(uint32_t st[8], const uint32_t w16[16]);
+
+// One launch of the plan.
+struct Piece {
+    uint64_t first;   // first nonce
+    uint64_t count;   // nonces
+    int kind;         // 0 fast, 1 generic
+    int digits;
+    int L;            // fast only
+    int J;            // fast only
+    int mode;         // fast only: FastMode
+    int blocks;       // tail blocks of the final message
+    FastArgs fa;      // kind 0
+    GenArgs ga;       // both (generic launch args; also used by hash_batch)
+};
+
+struct PlanOpts {
+    int lower_digits = 3;                        // L target
+    uint64_t max_nonces_per_launch = 1ull << 32; // bounds one launch to ~0.1 s
+};
+
+// Calls cb for every piece in increasing nonce order; stops early when cb
+// returns false.  lower <= upper required.
+void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
+                 const std::function<bool(const Piece&)>& cb);
+
+// Generic-kernel arguments for this prefix (first/count left 0).
+void make_gen_args(const Prefix& pre, GenArgs* ga);
+
+int decimal_digits(uint64_t n);
+
+}  // namespace mh

@@ -1,0 +1,387 @@
+// search_kernels.hip -- gfx950 kernels of libminehip.
+//
+// Hot path replaced: the miner's scan over bitcoin.Hash (reference
+// bitcoin/hash.go:13-17, scan spec SURVEY.md §8(a) A2 / stub
+// bitcoin/miner/miner.go:33).  Design: DESIGN.md §3.
+//
+//   fast_search<J, TWO>   one lane = one run of 10^L consecutive nonces that
+//                         share their d-L higher digits; the L lower digits
+//                         are enumerated in wave-uniform loops (digit
+//                         arithmetic is SALU); only message word J (the last
+//                         digit's word) changes per nonce, so the compiler
+//                         hoists rounds 0..J-1 and every schedule term that
+//                         does not depend on W[J] out of the per-nonce loop.
+//   generic_scan          one lane = one nonce, any layout (range edges,
+//                         buckets too small for runs).
+//   hash_batch            out[i] = Hash(msg, nonces[i]) (GPU bitcoin.Hash).
+//   merge_partials        folds per-workgroup (hash, nonce) candidates into
+//                         the search's running minimum (one workgroup).
+//
+// Every candidate comparison is the lexicographic (hash, nonce) order, which
+// equals the reference loop's strict-< first minimum.
+#include <hip/hip_runtime.h>
+
+#include "layout.hpp"
+#include "sha256_gfx950.hpp"
+
+namespace mh {
+namespace dev {
+
+__device__ __forceinline__ bool lex_less(uint64_t ha, uint64_t na, uint64_t hb, uint64_t nb) {
+    return ha < hb || (ha == hb && na < nb);
+}
+
+// Workgroup lexicographic min; the result is valid in thread 0.
+__device__ __forceinline__ void block_min(uint64_t& h, uint64_t& n) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t oh = __shfl_xor(h, off, 64);
+        const uint64_t on = __shfl_xor(n, off, 64);
+        if (lex_less(oh, on, h, n)) {
+            h = oh;
+            n = on;
+        }
+    }
+    __shared__ uint64_t sh[kBlockThreads / 64], sn[kBlockThreads / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) {
+        sh[wv] = h;
+        sn[wv] = n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 1; i < kBlockThreads / 64; ++i)
+            if (lex_less(sh[i], sn[i], h, n)) {
+                h = sh[i];
+                n = sn[i];
+            }
+    }
+}
+
+// w[wi] += v for a word index that is not a compile-time constant, without
+// dynamic register indexing (which would go to scratch).
+template <int NW>
+__device__ __forceinline__ void add_word(uint32_t (&w)[NW], uint32_t wi, uint32_t v) {
+#pragma unroll
+    for (int x = 0; x < NW; ++x) w[x] += (wi == (uint32_t)x) ? v : 0u;
+}
+
+// Rounds of a block whose message schedule is fully known on the host:
+// kw[i] = K[i] + W[i].  Returns only H0/H1 (feed-forward of words 0, 1).
+__device__ __forceinline__ void sha256_block_kw_h01(const uint32_t st[8], const uint32_t* kw, uint32_t& h0,
+                                                    uint32_t& h1) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw[i];
+        const uint32_t t2 = bsig0(a) + maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+    }
+    h0 = st[0] + a;
+    h1 = st[1] + b;
+}
+
+// Generic Hash(msg, n): formats n in registers and hashes the 1 or 2 tail
+// blocks from the host midstate.  Handles any digit count per lane.
+__device__ __forceinline__ void hash_generic(const GenArgs& a, uint64_t n, uint32_t& h0, uint32_t& h1) {
+    constexpr uint64_t P10[20] = {1ull, 10ull, 100ull, 1000ull, 10000ull, 100000ull, 1000000ull, 10000000ull,
+                                  100000000ull, 1000000000ull, 10000000000ull, 100000000000ull,
+                                  1000000000000ull, 10000000000000ull, 100000000000000ull,
+                                  1000000000000000ull, 10000000000000000ull, 100000000000000000ull,
+                                  1000000000000000000ull, 10000000000000000000ull};
+    uint32_t nd = 1;  // Go %d: no leading zeros, "0" for 0
+#pragma unroll
+    for (int k = 1; k < 20; ++k) nd += (n >= P10[k]) ? 1u : 0u;
+    uint32_t w[32];
+#pragma unroll
+    for (int x = 0; x < 16; ++x) w[x] = a.tail[x];
+#pragma unroll
+    for (int x = 16; x < 32; ++x) w[x] = 0u;
+    uint64_t u = n;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) {
+        if ((uint32_t)k < nd) {
+            const uint64_t q = u / 10u;
+            const uint32_t dg = (uint32_t)(u - q * 10u);
+            u = q;
+            const uint32_t pos = a.t + nd - 1u - (uint32_t)k;
+            add_word(w, pos >> 2, (0x30u + dg) << (24u - 8u * (pos & 3u)));
+        }
+    }
+    const uint32_t end = a.t + nd;  // tail length; the 0x80 byte goes here
+    add_word(w, end >> 2, 0x80u << (24u - 8u * (end & 3u)));
+    const uint64_t bits = (a.plen + nd) * 8u;
+    const bool two = end + 9u > 64u;
+    const uint32_t bhi = (uint32_t)(bits >> 32), blo = (uint32_t)bits;
+    w[14] = two ? w[14] : bhi;
+    w[15] = two ? w[15] : blo;
+    w[30] = two ? bhi : 0u;
+    w[31] = two ? blo : 0u;
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = a.mid[i];
+    if (!two) {
+        sha256_block_h01(st, w, h0, h1);
+    } else {
+        sha256_block(st, w);
+        sha256_block_h01(st, w + 16, h0, h1);
+    }
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------------------
+// fast_search<J, TWO>
+// ---------------------------------------------------------------------------
+// Which message-schedule words depend on word J (the only word that changes
+// from one nonce to the next inside a lane).  Bit t set <=> W[t] is
+// per-nonce.  Everything else is computed once per group (or per run) --
+// explicit hoisting: leaving it to LICM does not work because SROA turns the
+// message array into a loop-carried vector.
+template <int J>
+struct DepJ {
+    static constexpr uint64_t make() {
+        uint64_t m = 1ull << J;
+        for (int t = 16; t < 64; ++t)
+            if (((m >> (t - 2)) | (m >> (t - 7)) | (m >> (t - 15)) | (m >> (t - 16))) & 1ull) m |= 1ull << t;
+        return m;
+    }
+    static constexpr uint64_t kMask = make();
+};
+
+namespace dev {
+__device__ __forceinline__ void round_kw(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+                                         uint32_t& f, uint32_t& g, uint32_t& h, uint32_t kw) {
+    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+    const uint32_t t2 = bsig0(a) + maj(a, b, c);
+    h = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + t2;
+}
+}  // namespace dev
+
+template <int J, bool TWO>
+__global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, Partial* __restrict__ partials) {
+    using namespace dev;
+    constexpr uint32_t K[64] = MH_K256;
+    constexpr uint64_t DEP = DepJ<J>::kMask;
+#define MH_DEP(t) ((DEP >> (t)) & 1ull)
+    const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
+    const uint64_t U = a.u_start + gid;
+
+    // ---- per run --------------------------------------------------------
+    // Tail words: host template + the d-L digits of U, right-aligned so U's
+    // last digit sits at tail byte hi_end-1.
+    uint32_t w[32];
+#pragma unroll
+    for (int x = 0; x < 32; ++x) w[x] = a.blk[x];
+    {
+        uint64_t u = U;
+#pragma unroll
+        for (int k = 0; k < 20; ++k) {
+            if ((uint32_t)k < a.n_hi) {
+                const uint64_t q = u / 10u;
+                const uint32_t dg = (uint32_t)(u - q * 10u);
+                u = q;
+                const uint32_t pos = a.hi_end - 1u - (uint32_t)k;
+                add_word(w, pos >> 2, dg << (24u - 8u * (pos & 3u)));
+            }
+        }
+    }
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = a.mid[i];
+    uint32_t wb[16];
+    if (!TWO && a.mode == kModePre) {
+        sha256_block(st, w);  // tail block 0 holds no lower digit: once per run
+#pragma unroll
+        for (int x = 0; x < 16; ++x) wb[x] = w[16 + x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < 16; ++x) wb[x] = w[x];
+    }
+    // rounds 0..J-2 read only run-level words
+    uint32_t ra = st[0], rb = st[1], rc = st[2], rd = st[3], re = st[4], rf = st[5], rg = st[6], rh = st[7];
+#pragma unroll
+    for (int t = 0; t + 1 < J; ++t) round_kw(ra, rb, rc, rd, re, rf, rg, rh, K[t] + wb[t]);
+
+    const uint32_t lastpos = a.lo_pos + a.L - 1u;  // byte of the last digit, in word J
+    const uint32_t sh_last = 24u - 8u * (lastpos & 3u);
+    uint32_t bh0 = 0xFFFFFFFFu, bh1 = 0xFFFFFFFFu, bq = 0u;
+
+    for (uint32_t g = 0; g < a.n_groups; ++g) {
+        // ---- per group of 10 nonces --------------------------------------
+        // digits 0..L-2 of q = 10*g + i: wave-uniform, so this is SALU work
+        uint32_t cj = 0u, cjm = 0u, gg = g;
+        for (uint32_t k = a.L - 1u; k-- > 0u;) {
+            const uint32_t q = gg / 10u;
+            const uint32_t dg = gg - q * 10u;
+            gg = q;
+            const uint32_t p = a.lo_pos + k;
+            const uint32_t v = dg << (24u - 8u * (p & 3u));
+            if ((p >> 2) == (uint32_t)J)
+                cj += v;
+            else
+                cjm += v;
+        }
+        const uint32_t wJ = wb[J] + cj;
+        uint32_t wi[64];  // group-level schedule words (valid where !DEP)
+        uint32_t pi[64];  // group-level part of the per-nonce words
+#pragma unroll
+        for (int t = 0; t < 16; ++t) wi[t] = (t == J - 1) ? wb[t] + cjm : wb[t];
+#pragma unroll
+        for (int t = 16; t < 64; ++t) {
+            if (!MH_DEP(t)) {
+                wi[t] = (wi[t - 16] + wi[t - 7]) + ssig0(wi[t - 15]) + ssig1(wi[t - 2]);
+            } else {
+                uint32_t v = 0u;
+                if (!MH_DEP(t - 16)) v += wi[t - 16];
+                if (!MH_DEP(t - 7)) v += wi[t - 7];
+                if (!MH_DEP(t - 15)) v += ssig0(wi[t - 15]);
+                if (!MH_DEP(t - 2)) v += ssig1(wi[t - 2]);
+                pi[t] = v;
+            }
+        }
+        // round J-1 reads the group-level word J-1
+        uint32_t ga = ra, gb = rb, gc = rc, gd = rd, ge = re, gf = rf, gg2 = rg, gh = rh;
+        if constexpr (J > 0) round_kw(ga, gb, gc, gd, ge, gf, gg2, gh, K[J - 1] + wi[J - 1]);
+
+        for (uint32_t i = 0; i < 10u; ++i) {
+            // ---- per nonce ------------------------------------------------
+            uint32_t x[64];
+            x[J] = wJ + (i << sh_last);
+#pragma unroll
+            for (int t = 16; t < 64; ++t) {
+                if (MH_DEP(t)) {
+                    uint32_t v = pi[t];
+                    if (MH_DEP(t - 16)) v += x[t - 16];
+                    if (MH_DEP(t - 7)) v += x[t - 7];
+                    if (MH_DEP(t - 15)) v += ssig0(x[t - 15]);
+                    if (MH_DEP(t - 2)) v += ssig1(x[t - 2]);
+                    x[t] = v;
+                }
+            }
+            uint32_t A = ga, B = gb, C = gc, D = gd, E = ge, F = gf, G = gg2, H = gh;
+#pragma unroll
+            for (int t = J; t < 64; ++t) round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_DEP(t) ? x[t] : wi[t]));
+            uint32_t h0, h1;
+            if constexpr (!TWO) {
+                h0 = st[0] + A;
+                h1 = st[1] + B;
+            } else {
+                uint32_t s2[8] = {st[0] + A, st[1] + B, st[2] + C, st[3] + D,
+                                  st[4] + E, st[5] + F, st[6] + G, st[7] + H};
+                sha256_block_kw_h01(s2, a.kw1, h0, h1);  // block 1: padding + length only
+            }
+            if (h0 <= bh0) {
+                if (h0 < bh0 || h1 < bh1) {
+                    bh0 = h0;
+                    bh1 = h1;
+                    bq = g * 10u + i;
+                }
+            }
+        }
+    }
+#undef MH_DEP
+
+    uint64_t hash = ((uint64_t)bh0 << 32) | bh1;
+    uint64_t nonce = U * a.pow10L + bq;
+    if (gid >= a.n_runs) {
+        hash = ~0ull;
+        nonce = ~0ull;
+    }
+    block_min(hash, nonce);
+    if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
+}
+
+__global__ __launch_bounds__(kBlockThreads) void generic_scan(const GenArgs a, Partial* __restrict__ partials) {
+    using namespace dev;
+    const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
+    const uint64_t n = a.first + gid;
+    uint32_t h0, h1;
+    hash_generic(a, n, h0, h1);
+    uint64_t hash = ((uint64_t)h0 << 32) | h1, nonce = n;
+    if (gid >= a.count) {
+        hash = ~0ull;
+        nonce = ~0ull;
+    }
+    block_min(hash, nonce);
+    if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
+}
+
+__global__ __launch_bounds__(kBlockThreads) void hash_batch(const GenArgs a, const uint64_t* __restrict__ nonces,
+                                                            uint64_t* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+    if (i >= n) return;
+    uint32_t h0, h1;
+    dev::hash_generic(a, nonces[i], h0, h1);
+    out[i] = ((uint64_t)h0 << 32) | h1;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void merge_partials(const Partial* __restrict__ p, uint32_t n,
+                                                                Partial* __restrict__ best) {
+    using namespace dev;
+    uint64_t h = ~0ull, nn = ~0ull;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlockThreads) {
+        const Partial x = p[i];
+        if (lex_less(x.hash, x.nonce, h, nn)) {
+            h = x.hash;
+            nn = x.nonce;
+        }
+    }
+    block_min(h, nn);
+    if (threadIdx.x == 0) {
+        const Partial b = *best;
+        if (lex_less(h, nn, b.hash, b.nonce)) *best = Partial{h, nn};
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+template <int J, bool TWO>
+static hipError_t launch_fast_t(const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL((fast_search<J, TWO>), dim3(blocks), dim3(kBlockThreads), 0, s, a, partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast(int J, bool two, const FastArgs& a, Partial* partials,
+                       uint32_t blocks, hipStream_t s) {
+    if (!two) {
+        switch (J) {
+#define MH_CASE(j) \
+    case j:        \
+        return launch_fast_t<j, false>(a, partials, blocks, s);
+            MH_CASE(0) MH_CASE(1) MH_CASE(2) MH_CASE(3) MH_CASE(4) MH_CASE(5) MH_CASE(6)
+            MH_CASE(7) MH_CASE(8) MH_CASE(9) MH_CASE(10) MH_CASE(11) MH_CASE(12) MH_CASE(13)
+#undef MH_CASE
+            default: return hipErrorInvalidValue;
+        }
+    }
+    switch (J) {
+        case 13: return launch_fast_t<13, true>(a, partials, blocks, s);
+        case 14: return launch_fast_t<14, true>(a, partials, blocks, s);
+        case 15: return launch_fast_t<15, true>(a, partials, blocks, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(generic_scan, dim3(blocks), dim3(kBlockThreads), 0, s, a, partials);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
+                             hipStream_t s) {
+    const uint64_t blocks = (n + kBlockThreads - 1) / kBlockThreads;
+    hipLaunchKernelGGL(hash_batch, dim3((uint32_t)blocks), dim3(kBlockThreads), 0, s, a, d_nonces, d_out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const Partial* partials, uint32_t n, Partial* best, hipStream_t s) {
+    hipLaunchKernelGGL(merge_partials, dim3(1), dim3(kBlockThreads), 0, s, partials, n, best);
+    return hipGetLastError();
+}
+
+}  // namespace mh

@@ -1,0 +1,171 @@
+"""minehip -- MI355X (gfx950) SHA-256 nonce search for the CMU 15-440 miner.
+
+Python face of libminehip.so, named after the reference's own API so parity
+tests read like the reference (line numbers into the reference repo):
+
+  Hash(msg, nonce)           bitcoin/hash.go:13-17, computed on the GPU
+  hash_batch(msg, nonces)    the same for many nonces
+  search(msg, lower, upper)  the miner scan (stub miner.go:33)
+  search_multi(...)          the scan sharded over several devices
+  Message / NewRequest / NewResult / NewJoin / marshal / unmarshal
+                             bitcoin/message.go:7-62 with Go encoding/json bytes
+  miner_handle(request)      one miner step: Request payload -> Result payload
+
+All compute goes through the C-ABI; there is no host fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib, mh_piece, mh_message, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
+from ._lib import MH_OK, MH_EINVAL, MH_ERANGE, MH_ETOOLONG, MH_ENODEV, MH_EHIP  # noqa: F401
+
+U64_MAX = (1 << 64) - 1
+
+
+class MinehipError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"minehip error {code}: {what}")
+        self.code = code
+
+
+def _check(rc):
+    if rc != MH_OK:
+        raise MinehipError(rc, lib.mh_last_error().decode("utf-8", "replace"))
+
+
+def _b(msg):
+    return msg.encode("utf-8") if isinstance(msg, str) else bytes(msg)
+
+
+def device_count():
+    return lib.mh_device_count()
+
+
+def search(msg, lower, upper, dev=0):
+    """(hash, nonce) = lexicographic min of (Hash(msg, n), n), n in [lower, upper]."""
+    m = _b(msg)
+    h = ctypes.c_uint64()
+    n = ctypes.c_uint64()
+    _check(lib.mh_search(dev, m, len(m), lower, upper, ctypes.byref(h), ctypes.byref(n)))
+    return h.value, n.value
+
+
+def search_multi(msg, lower, upper, devs=None, chunk=0):
+    m = _b(msg)
+    if devs is None:
+        devs = list(range(device_count()))
+    arr = (ctypes.c_int * len(devs))(*devs)
+    h = ctypes.c_uint64()
+    n = ctypes.c_uint64()
+    _check(lib.mh_search_multi(arr, len(devs), m, len(m), lower, upper, chunk, ctypes.byref(h),
+                               ctypes.byref(n)))
+    return h.value, n.value
+
+
+def hash_batch(msg, nonces, dev=0):
+    m = _b(msg)
+    a = np.ascontiguousarray(nonces, dtype=np.uint64)
+    out = np.empty_like(a)
+    p = ctypes.POINTER(ctypes.c_uint64)
+    _check(lib.mh_hash_batch(dev, m, len(m), a.ctypes.data_as(p), a.size, out.ctypes.data_as(p)))
+    return out
+
+
+def Hash(msg, nonce, dev=0):  # noqa: N802  (reference name, bitcoin/hash.go:13)
+    return int(hash_batch(msg, [nonce], dev)[0])
+
+
+def plan(msg, lower, upper, cap=1 << 16):
+    """Host-only: the launch plan of a search (list of dicts)."""
+    m = _b(msg)
+    buf = (mh_piece * cap)()
+    k = lib.mh_plan(m, len(m), lower, upper, buf, cap)
+    if k < 0:
+        _check(k)
+    if k > cap:
+        raise ValueError("plan longer than cap")
+    return [{f: getattr(buf[i], f) for f, _ in mh_piece._fields_} for i in range(k)]
+
+
+def profile_enable(dev=0, on=True):
+    _check(lib.mh_profile_enable(dev, 1 if on else 0))
+
+
+def profile_read(dev=0):
+    out = (ctypes.c_uint64 * 8)()
+    _check(lib.mh_profile_read(dev, out, 8))
+    keys = ("fast_launches", "fast_nonces", "fast_ns", "fast_ops", "generic_nonces", "generic_ns")
+    return {k: int(out[i]) for i, k in enumerate(keys)}
+
+
+# ---- bitcoin/message.go mirror --------------------------------------------
+Join, Request, Result = 0, 1, 2  # MsgType iota, message.go:9-13
+
+
+class Message:
+    """bitcoin.Message (message.go:18-23)."""
+
+    __slots__ = ("Type", "Data", "Lower", "Upper", "Hash", "Nonce")
+
+    def __init__(self, Type=0, Data=b"", Lower=0, Upper=0, Hash=0, Nonce=0):  # noqa: N803
+        self.Type, self.Data = Type, _b(Data)
+        self.Lower, self.Upper, self.Hash, self.Nonce = Lower, Upper, Hash, Nonce
+
+    def __eq__(self, o):
+        return isinstance(o, Message) and all(getattr(self, k) == getattr(o, k) for k in self.__slots__)
+
+    def __repr__(self):
+        return self.String()
+
+    def String(self):  # noqa: N802  (message.go:51-62)
+        if self.Type == Request:
+            return "[Request %s %d %d]" % (self.Data.decode("utf-8", "replace"), self.Lower, self.Upper)
+        if self.Type == Result:
+            return "[Result %d %d]" % (self.Hash, self.Nonce)
+        if self.Type == Join:
+            return "[Join]"
+        return ""
+
+
+def NewRequest(data, lower, upper):  # noqa: N802  (message.go:27-34)
+    return Message(Request, data, lower, upper)
+
+
+def NewResult(hash_, nonce):  # noqa: N802  (message.go:38-44)
+    return Message(Result, b"", 0, 0, hash_, nonce)
+
+
+def NewJoin():  # noqa: N802  (message.go:47-49)
+    return Message(Join)
+
+
+def marshal(m):
+    """json.Marshal(m) as Go produces it."""
+    need = ctypes.c_size_t()
+    lib.mh_msg_encode(m.Type, m.Data, len(m.Data), m.Lower, m.Upper, m.Hash, m.Nonce, None, 0,
+                      ctypes.byref(need))
+    buf = ctypes.create_string_buffer(need.value)
+    _check(lib.mh_msg_encode(m.Type, m.Data, len(m.Data), m.Lower, m.Upper, m.Hash, m.Nonce, buf,
+                             need.value, ctypes.byref(need)))
+    return buf.raw[:need.value]
+
+
+def unmarshal(payload):
+    """json.Unmarshal(payload, &m) with Go's decoding rules."""
+    p = _b(payload)
+    mm = mh_message()
+    cap = len(p) + 16
+    data = ctypes.create_string_buffer(cap)
+    _check(lib.mh_msg_decode(p, len(p), ctypes.byref(mm), data, cap))
+    return Message(mm.type, data.raw[:mm.data_len], mm.lower, mm.upper, mm.hash, mm.nonce)
+
+
+def miner_handle(request_payload, devs=(0,)):
+    """One GPU-miner step: Request payload -> Result payload (both Go JSON)."""
+    p = _b(request_payload)
+    arr = (ctypes.c_int * len(devs))(*devs)
+    need = ctypes.c_size_t()
+    buf = ctypes.create_string_buffer(256)
+    _check(lib.mh_miner_handle(arr, len(devs), p, len(p), buf, 256, ctypes.byref(need)))
+    return buf.raw[:need.value]

@@ -1,0 +1,72 @@
+"""ctypes binding of libminehip.so (C-ABI: include/minehip.h).
+
+The library is built in-tree (``make`` at the repo root, or
+``__graft_entry__.build()``) next to this file.  There is no fallback: if the
+shared object is missing, importing this module raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libminehip.so")
+
+MH_OK = 0
+MH_EINVAL = -1
+MH_ERANGE = -2
+MH_ETOOLONG = -3
+MH_ENODEV = -4
+MH_EHIP = -5
+OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
+
+#: every symbol include/minehip.h declares
+EXPORTS = (
+    "mh_abi_version", "mh_device_count", "mh_search", "mh_search_multi", "mh_hash_batch",
+    "mh_last_error", "mh_msg_encode", "mh_msg_decode", "mh_miner_handle",
+    "mh_profile_enable", "mh_profile_read", "mh_plan",
+)
+
+
+class mh_piece(ctypes.Structure):
+    _fields_ = [("first", ctypes.c_uint64), ("count", ctypes.c_uint64), ("kind", ctypes.c_int32),
+                ("digits", ctypes.c_int32), ("lo_digits", ctypes.c_int32), ("word", ctypes.c_int32),
+                ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32)]
+
+
+class mh_message(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int64), ("lower", ctypes.c_uint64), ("upper", ctypes.c_uint64),
+                ("hash", ctypes.c_uint64), ("nonce", ctypes.c_uint64), ("data_len", ctypes.c_size_t)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libminehip.so not found at {LIB_PATH}; build it with `make` at the repo root "
+            "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.c_char_p
+    sz = ctypes.c_size_t
+    u64 = ctypes.c_uint64
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    intp = ctypes.POINTER(ctypes.c_int)
+    L.mh_abi_version.restype = ctypes.c_int
+    L.mh_device_count.restype = ctypes.c_int
+    L.mh_last_error.restype = ctypes.c_char_p
+    L.mh_search.argtypes = [ctypes.c_int, u8p, sz, u64, u64, u64p, u64p]
+    L.mh_search_multi.argtypes = [intp, ctypes.c_int, u8p, sz, u64, u64, u64, u64p, u64p]
+    L.mh_hash_batch.argtypes = [ctypes.c_int, u8p, sz, u64p, sz, u64p]
+    L.mh_msg_encode.argtypes = [ctypes.c_int64, u8p, sz, u64, u64, u64, u64, ctypes.c_char_p, sz,
+                                ctypes.POINTER(sz)]
+    L.mh_msg_decode.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(mh_message), ctypes.c_char_p, sz]
+    L.mh_miner_handle.argtypes = [intp, ctypes.c_int, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
+                                  ctypes.POINTER(sz)]
+    L.mh_profile_enable.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.mh_profile_read.argtypes = [ctypes.c_int, u64p, ctypes.c_int]
+    L.mh_plan.argtypes = [u8p, sz, u64, u64, ctypes.POINTER(mh_piece), ctypes.c_int64]
+    L.mh_plan.restype = ctypes.c_int64
+    for name in EXPORTS:
+        if name not in ("mh_plan", "mh_last_error"):
+            getattr(L, name).restype = ctypes.c_int
+    return L
+
+
+lib = _load()

@@ -1,0 +1,184 @@
+"""CPU tests of the C-ABI library: load, exports, argument/error behaviour,
+the launch planner (host-only) and the bitcoin.Message codec.  No GPU compute
+is called here."""
+import ctypes
+import os
+import random
+import re
+
+import pytest
+
+import minehip
+from minehip import _lib
+from conftest import ROOT
+
+U64 = (1 << 64) - 1
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "minehip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mh_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    syms = header_symbols()
+    assert set(syms) == set(_lib.EXPORTS)
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for s in syms:
+        assert hasattr(raw, s), s
+
+
+def test_abi_version_and_devices():
+    assert minehip.lib.mh_abi_version() == 1
+    assert minehip.device_count() >= 0
+
+
+def test_no_device_fails_loudly():
+    if minehip.device_count() > 0:
+        pytest.skip("a device is visible")
+    with pytest.raises(minehip.MinehipError) as e:
+        minehip.search("cmu440", 0, 10)
+    assert e.value.code == minehip.MH_ENODEV
+    with pytest.raises(minehip.MinehipError):
+        minehip.hash_batch("cmu440", [1, 2, 3])
+
+
+def test_argument_errors():
+    h = ctypes.c_uint64()
+    n = ctypes.c_uint64()
+    rc = minehip.lib.mh_search(0, b"x", 1, 5, 4, ctypes.byref(h), ctypes.byref(n))
+    assert rc == minehip.MH_ERANGE
+    rc = minehip.lib.mh_search(0, b"x", 1, 0, 4, None, ctypes.byref(n))
+    assert rc == minehip.MH_EINVAL
+    assert b"NULL" in minehip.lib.mh_last_error()
+    rc = minehip.lib.mh_search(0, None, 3, 0, 4, ctypes.byref(h), ctypes.byref(n))
+    assert rc == minehip.MH_EINVAL
+    with pytest.raises(minehip.MinehipError) as e:
+        minehip.plan("x", 9, 3)
+    assert e.value.code == minehip.MH_ERANGE
+
+
+# ---- planner ---------------------------------------------------------------
+
+def digits(n):
+    return len(str(n))
+
+
+def check_plan(msg, lo, hi):
+    pieces = minehip.plan(msg, lo, hi)
+    assert pieces, "empty plan"
+    cur = lo
+    plen = len(msg) + 1
+    for p in pieces:
+        assert p["first"] == cur, (msg, lo, hi, p)
+        assert p["count"] >= 1
+        last = p["first"] + p["count"] - 1
+        assert last <= hi
+        d = p["digits"]
+        assert digits(p["first"]) == d and digits(last) == d, p  # one decimal bucket per piece
+        t = plen % 64
+        assert p["blocks"] == (1 if t + d + 9 <= 64 else 2)
+        if p["kind"] == 0:
+            L = p["lo_digits"]
+            R = 10 ** L
+            assert 1 <= L <= min(5, d - 1)
+            assert p["first"] % R == 0 and p["count"] % R == 0  # whole runs only
+            pl = t + d - 1
+            base = 64 if (p["blocks"] == 2 and pl >= 64) else 0
+            assert p["word"] == (pl - base) >> 2
+            assert ((pl - base - L + 1) >> 2) >= p["word"] - 1
+            if p["mode"] == 1:
+                assert pl - L + 1 >= 64
+            if p["mode"] == 2:
+                assert pl < 64 and 13 <= p["word"] <= 15
+        cur = last + 1
+    assert cur - 1 == hi
+    return pieces
+
+
+def test_plan_covers_exactly():
+    rng = random.Random(440)
+    msgs = [b"", b"cmu440", b"x" * 54, b"x" * 55, b"x" * 60, b"a" * 100, b"y" * 127, b"z" * 600]
+    msgs += [bytes(rng.choice(b"abc ") for _ in range(L)) for L in range(0, 130, 3)]
+    for m in msgs:
+        check_plan(m, 0, 2 ** 32 - 1)
+        check_plan(m, 0, 0)
+        check_plan(m, U64 - 12345, U64)
+        check_plan(m, U64, U64)
+        for _ in range(4):
+            k = rng.randrange(1, 20)
+            lo = max(0, 10 ** k - rng.randrange(0, 10 ** min(k, 6)))
+            hi = min(U64, lo + rng.randrange(0, 10 ** 7))
+            check_plan(m, lo, hi)
+
+
+def test_plan_uses_fast_kernel_for_bulk():
+    pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
+    fast = sum(p["count"] for p in pieces if p["kind"] == 0)
+    assert fast / 2 ** 32 > 0.9999
+    # long message, digits in the second tail block: per-run prefix block
+    pieces = check_plan(b"x" * 60, 0, 2 ** 34 - 1)
+    assert {p["mode"] for p in pieces if p["kind"] == 0} >= {1}
+    assert sum(p["count"] for p in pieces if p["kind"] == 0) / 2 ** 34 > 0.9999
+
+
+def test_plan_launch_cap():
+    pieces = check_plan(b"cmu440", 0, 2 ** 40 - 1)
+    assert max(p["count"] for p in pieces) <= 2 ** 32
+
+
+# ---- bitcoin.Message codec (Go encoding/json bytes) ------------------------
+
+GO_JSON = [
+    (minehip.NewJoin(), b'{"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}'),
+    (minehip.NewRequest("cmu440", 0, 9999999),
+     b'{"Type":1,"Data":"cmu440","Lower":0,"Upper":9999999,"Hash":0,"Nonce":0}'),
+    (minehip.NewResult(1228377698034, 1067492),
+     b'{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":1228377698034,"Nonce":1067492}'),
+    (minehip.NewRequest('a"b\\c\n\t\r<>&\x01', 0, U64),
+     b'{"Type":1,"Data":"a\\"b\\\\c\\n\\t\\r\\u003c\\u003e\\u0026\\u0001","Lower":0,'
+     b'"Upper":18446744073709551615,"Hash":0,"Nonce":0}'),
+    (minehip.NewRequest("héllo ✓ 世 ", 1, 2),
+     '{"Type":1,"Data":"héllo ✓ 世\\u2028","Lower":1,"Upper":2,"Hash":0,"Nonce":0}'.encode()),
+]
+
+
+def test_marshal_matches_go():
+    for m, js in GO_JSON:
+        assert minehip.marshal(m) == js
+
+
+def test_marshal_invalid_utf8():
+    m = minehip.Message(minehip.Request, b"\xff\xfeok", 0, 1)
+    assert minehip.marshal(m) == b'{"Type":1,"Data":"\\ufffd\\ufffdok","Lower":0,"Upper":1,"Hash":0,"Nonce":0}'
+
+
+def test_unmarshal_roundtrip_and_go_rules():
+    for m, js in GO_JSON:
+        assert minehip.unmarshal(js) == m
+    # case-insensitive keys, unknown keys, whitespace, escapes, key order
+    m = minehip.unmarshal(b' { "upper" : 7 , "extra": [1, {"a": null}], "TYPE":1, "data":"x\\u00e9\\ud83d\\ude00",'
+                          b' "lower":3 } ')
+    assert m == minehip.Message(1, "xé\U0001F600", 3, 7)
+    with pytest.raises(minehip.MinehipError):
+        minehip.unmarshal(b'{"Type":1,"Lower":-1}')
+    with pytest.raises(minehip.MinehipError):
+        minehip.unmarshal(b'{"Lower":18446744073709551616}')
+    with pytest.raises(minehip.MinehipError):
+        minehip.unmarshal(b'not json')
+
+
+def test_message_string():
+    assert minehip.NewRequest("cmu440", 0, 9).String() == "[Request cmu440 0 9]"
+    assert minehip.NewResult(5, 6).String() == "[Result 5 6]"
+    assert minehip.NewJoin().String() == "[Join]"
+
+
+def test_miner_handle_rejects_non_requests():
+    with pytest.raises(minehip.MinehipError) as e:
+        minehip.miner_handle(minehip.marshal(minehip.NewJoin()))
+    assert e.value.code == minehip.MH_EINVAL
+    with pytest.raises(minehip.MinehipError) as e:
+        minehip.miner_handle(minehip.marshal(minehip.NewRequest("x", 9, 1)))
+    assert e.value.code == minehip.MH_ERANGE

@@ -1,0 +1,167 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the
+golden fixtures.  Bit-exact (integer work).  Reference semantics:
+bitcoin/hash.go:13-17 (Hash) and the miner scan spec (SURVEY.md §8(a) A2,
+reference stub bitcoin/miner/miner.go:33).
+
+Small sizes are checked element for element against oracle/; BASELINE.json's
+full sizes (2^32 and 2^34 nonces) are checked through size-independent
+properties: split-range associativity of the min, invariance to the launch
+plan (lower-digit count L, launch size, device chunking), and that the
+reported (hash, nonce) re-hashes to itself.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+U64 = (1 << 64) - 1
+
+
+def lexmin(a, b):
+    return a if a <= b else b
+
+
+class env:
+    """Temporarily set planner knobs (read by libminehip on every search)."""
+
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_hash_batch_golden(gpu, golden_hash):
+    by_msg = {}
+    for m, n, h in golden_hash:
+        by_msg.setdefault(m, []).append((n, h))
+    for m, lst in by_msg.items():
+        got = gpu.hash_batch(m, np.array([n for n, _ in lst], dtype=np.uint64))
+        exp = np.array([h for _, h in lst], dtype=np.uint64)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (m[:20], [lst[i] for i in bad[:3]])
+
+
+def test_hash_single(gpu):
+    assert gpu.Hash("cmu440", 0) == 11864962392530079502
+    assert gpu.Hash("cmu440", U64) == 12656178859598403723
+    assert gpu.Hash("", 0) == 17297653956949303043
+
+
+def test_hash_batch_random_vs_oracle(gpu):
+    rng = np.random.default_rng(440)
+    for L in (0, 1, 7, 54, 55, 56, 62, 63, 64, 118, 119, 200, 601):
+        m = bytes(rng.integers(32, 127, size=L, dtype=np.uint8))
+        nonces = rng.integers(0, U64, size=5000, dtype=np.uint64, endpoint=True)
+        nonces[:20] = [10 ** k for k in range(20)]
+        assert (gpu.hash_batch(m, nonces) == oracle.hash_batch(m, nonces)).all(), L
+    assert gpu.hash_batch("x", []).size == 0
+
+
+def test_scan_golden(gpu, golden_scan):
+    small, big = golden_scan
+    for m, lo, hi, h, n in small:
+        assert gpu.search(m, lo, hi) == (h, n), (m[:16], lo, hi)
+
+
+def test_config1(gpu, golden_scan):
+    """BASELINE.json configs[0]: "cmu440", nonces 0..9,999,999."""
+    _, big = golden_scan
+    m, lo, hi, h, n = big[0]
+    assert gpu.search(m, lo, hi) == (h, n) == (1228377698034, 1067492)
+
+
+def test_every_tail_offset_and_bucket(gpu):
+    """Every prefix length mod 64 (all fast-kernel layouts J / modes) and
+    ranges straddling 10^k for many k, against the oracle."""
+    rng = random.Random(440)
+    for L in range(0, 131):
+        m = bytes(rng.choice(b"abcdefghij ") for _ in range(L))
+        for k in rng.sample(range(2, 20), 3) + [19]:
+            c = 10 ** k
+            lo = max(0, c - rng.randrange(1000, 9000))
+            hi = min(U64, c + rng.randrange(3000, 14000))
+            assert gpu.search(m, lo, hi) == oracle.search(m, lo, hi, threads=8), (L, lo, hi)
+
+
+def test_u64_edges(gpu):
+    for m in (b"cmu440", b"", b"q" * 60, b"r" * 119):
+        assert gpu.search(m, U64, U64) == (oracle.hash_(m, U64), U64)
+        assert gpu.search(m, U64 - 30000, U64) == oracle.search(m, U64 - 30000, U64, threads=8)
+        assert gpu.search(m, 0, 0) == (oracle.hash_(m, 0), 0)
+        assert gpu.search(m, 0, 25000) == oracle.search(m, 0, 25000, threads=8)
+
+
+def test_long_messages(gpu):
+    for L in (191, 192, 300, 447, 600, 1000, 5000):
+        m = bytes((i * 7 + 3) % 95 + 32 for i in range(L))
+        assert gpu.search(m, 999000, 1012000) == oracle.search(m, 999000, 1012000, threads=8), L
+
+
+def test_plan_invariance_small(gpu):
+    """The result must not depend on how the range is cut into launches."""
+    for m, lo, hi in ((b"cmu440", 0, 2_000_000), (b"x" * 60, 10 ** 9 - 7, 10 ** 9 + 600_000),
+                      (b"a" * 100, 123, 345_678), (b"y" * 52, 10 ** 12 - 50_000, 10 ** 12 + 50_000)):
+        exp = oracle.search(m, lo, hi, threads=8)
+        for Ld in (1, 2, 3, 4, 5):
+            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_LAUNCH_NONCES=100_000):
+                assert gpu.search(m, lo, hi) == exp, (m[:8], Ld)
+
+
+@pytest.mark.parametrize("msg,bits", [(b"cmu440", 32), (b"a" * 100, 34), (b"x" * 60, 34)])
+def test_full_size_properties(gpu, msg, bits):
+    """BASELINE configs[1] (2^32 nonces, single block) and configs[2]
+    (long messages over 2^34: host midstate / two tail blocks)."""
+    hi = (1 << bits) - 1
+    r = gpu.search(msg, 0, hi)
+    assert oracle.hash_(msg, r[1]) == r[0] and 0 <= r[1] <= hi  # re-hashes to itself
+    rng = random.Random(bits)
+    for _ in range(2):  # split-range associativity
+        mid = rng.randrange(1, hi)
+        assert lexmin(gpu.search(msg, 0, mid), gpu.search(msg, mid + 1, hi)) == r
+    with env(MINEHIP_LOWER_DIGITS=4):
+        assert gpu.search(msg, 0, hi) == r
+    with env(MINEHIP_LOWER_DIGITS=2, MINEHIP_LAUNCH_NONCES=1 << 28):
+        assert gpu.search(msg, 0, hi) == r
+    assert gpu.search_multi(msg, 0, hi, devs=[0, 0, 0], chunk=(1 << bits) // 7 + 3) == r
+    # no sampled nonce beats it (oracle on 200k random nonces of the range)
+    sample = np.random.default_rng(bits).integers(0, hi, size=200_000, dtype=np.uint64, endpoint=True)
+    hs = oracle.hash_batch(msg, sample)
+    assert int(hs.min()) >= r[0]
+
+
+def test_miner_handle(gpu):
+    req = gpu.marshal(gpu.NewRequest("cmu440", 0, 9999999))
+    res = gpu.miner_handle(req)
+    assert res == b'{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":1228377698034,"Nonce":1067492}'
+    assert gpu.unmarshal(res) == gpu.NewResult(1228377698034, 1067492)
+
+
+def test_search_multi_matches(gpu):
+    for m, lo, hi in ((b"cmu440", 5, 3_000_000), (b"z" * 70, U64 - 2_000_000, U64)):
+        exp = gpu.search(m, lo, hi)
+        assert gpu.search_multi(m, lo, hi, devs=[0, 0], chunk=123_457) == exp
+        assert gpu.search_multi(m, lo, hi, devs=[0]) == exp
+
+
+def test_profile_counters(gpu):
+    gpu.profile_enable(0, True)
+    gpu.search("cmu440", 0, (1 << 30) - 1)
+    p = gpu.profile_read(0)
+    gpu.profile_enable(0, False)
+    assert p["fast_launches"] >= 1 and p["fast_ns"] > 0
+    assert p["fast_nonces"] + p["generic_nonces"] == 1 << 30
+    assert p["fast_ops"] == p["fast_nonces"] * 1376

@@ -1,0 +1,69 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprof kernel-trace summary.
+# Each GPU step runs under its own timeout; after a crash / abort / timeout
+# (exit 124, 134, 137, 139 or >128) nothing else touches the GPU.
+# Usage (from the repo root on the box): bash tools/gpu_session.sh [TAG] [STEPS...]
+#   STEPS default: info tests bench prof
+set -u
+TAG=${1:-r01}; shift || true
+STEPS=${*:-info tests bench prof}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+fatal() { # exit code -> 0 if it is safe to continue on the GPU
+  local rc=$1
+  if [ "$rc" -eq 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 137 ] || [ "$rc" -eq 139 ] || [ "$rc" -gt 128 ]; then
+    echo "GPU step ended with $rc: stopping the session" | tee -a "$OUT/session.log"; exit "$rc"
+  fi
+}
+
+for s in $STEPS; do
+  echo "== $s $(date +%T)" | tee -a "$OUT/session.log"
+  case $s in
+    info)
+      (rocminfo 2>&1 | grep -E 'Marketing Name|Name: +gfx|Compute Unit|Max Clock|SIMDs per CU' | head -20
+       nproc; grep -m1 'model name' /proc/cpuinfo; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}"
+       (go version || echo "no go") 2>&1
+       amd-smi static --clock 2>/dev/null | head -40) > "$OUT/info.txt" 2>&1
+      ;;
+    build)
+      make -C "$ROOT" -j16 all > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 1; }
+      ;;
+    tests)
+      timeout -k 10 900 python -m pytest "$ROOT/tests" -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+      rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/pytest_gpu.log"; fatal $rc
+      ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      ;;
+    bench)
+      timeout -k 10 600 python "$ROOT/bench.py" --steps 5 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err"
+      rc=$?; echo "bench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench.json"; fatal $rc
+      ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+          -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+      rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
+      ;;
+    pmc)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
+          -d "$OUT/pmc1" -o run --output-format csv \
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc1.err")
+      rc=$?; echo "pmc1 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace \
+          -d "$OUT/pmc2" -o run --output-format csv \
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc2.err")
+      rc=$?; echo "pmc2 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
+          -d "$OUT/pmc3" -o run --output-format csv \
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc3.err")
+      rc=$?; echo "pmc3 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      ;;
+    *) echo "unknown step $s";;
+  esac
+done
+echo "== done $(date +%T)" | tee -a "$OUT/session.log"
