@@ -30,8 +30,11 @@ for _p in (ROOT, os.path.join(ROOT, "bitcoin-miner_amd")):
 
 METRIC = "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of VALU int roofline"
 PEAK_SCLK_HZ = 2.4e9          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
-LANES_PER_CU_CLK = 4 * 32     # 4 SIMD-32 per CU: a wave64 VALU op issues in 2 cycles
-OPS_PER_BLOCK = 1376          # canonical gfx950 VALU ops per SHA-256 compression
+# Integer VALU issue for SHA-256's instruction mix: 64 lanes/clk/CU.  Half-rate
+# 3-input ops (v_alignbit, v_add3) and any stream mixing them issue at this rate
+# (tools/valu_ops.hip, tools/gen_valu_mix.py).
+LANES_PER_CU_CLK = 64
+OPS_PER_BLOCK = 1376          # gfx950 VALU instructions of one un-hoisted SHA-256 compression
 
 
 def shard(rank, bits):
@@ -156,6 +159,7 @@ def main():
     props = torch.cuda.get_device_properties(device)
     cus = int(props.multi_processor_count)
     peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
+    # algorithmic lane-instructions: sum over fast launches of nonces x nonce_ops (x 64 lanes / 64 nonces)
     achieved = prof["fast_ops"] / (prof["fast_ns"] * 1e-9) / 1e12 if prof["fast_ns"] else 0.0
     launches = max(1, prof["fast_launches"])
 
@@ -187,11 +191,12 @@ def main():
                 "bound": "valu",
                 "achieved": round(achieved, 3),
                 "peak": round(peak, 3),
-                "unit": "TOPS (int32 VALU)",
+                "unit": "T int32 VALU lane-instructions/s",
                 "frac": round(achieved / peak, 4) if peak else None,
                 "traffic": None,
                 "kernel": "fast_search",
-                "ops_per_nonce": OPS_PER_BLOCK,
+                "ops_per_nonce": round(prof["fast_ops"] / max(1, prof["fast_nonces"]), 1),
+                "full_compression_ops": OPS_PER_BLOCK,
                 "avg_launch_ms": round(prof["fast_ns"] / launches / 1e6, 4),
                 "launches": prof["fast_launches"],
                 "kernel_ghs": round(prof["fast_nonces"] / (prof["fast_ns"] * 1e-9) / 1e9, 4)

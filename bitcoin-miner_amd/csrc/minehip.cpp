@@ -22,7 +22,7 @@
 #include "plan.hpp"
 
 namespace mh {
-hipError_t launch_fast(int J, bool two, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
+hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
                              hipStream_t s);
@@ -161,7 +161,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
             return fail(MH_EINVAL, "internal: bad fast piece");
         blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
         if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINVAL, "internal: fast grid too large");
-        MH_HIP(mh::launch_fast(p.J, p.mode == mh::kModeTwo, p.fa, c->d_partials, blocks, c->stream));
+        MH_HIP(mh::launch_fast(p.J, p.mode, p.fa, c->d_partials, blocks, c->stream));
     } else {
         if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
             return fail(MH_EINVAL, "internal: bad generic piece");
@@ -174,7 +174,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
         if (p.kind == 0) {
             c->cnt[0] += 1;
             c->cnt[1] += p.count;
-            c->cnt[3] += p.count * (uint64_t)p.blocks * (uint64_t)MH_OPS_PER_BLOCK;
+            c->cnt[3] += p.count * (uint64_t)p.ops;
         } else {
             c->cnt[4] += p.count;
         }
@@ -185,6 +185,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
 // Planner knobs, overridable for tests and tuning (the result never depends
 // on them -- tests/test_gpu_parity.py checks exactly that):
 //   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 3)
+//   MINEHIP_MIN_LANES      lower L per bucket until it has this many runs (2^18)
 //   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^32)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
@@ -192,6 +193,7 @@ mh::PlanOpts plan_opts() {
         const int v = atoi(e);
         if (v >= 1 && v <= 5) o.lower_digits = v;
     }
+    if (const char* e = getenv("MINEHIP_MIN_LANES")) o.min_lanes = strtoull(e, nullptr, 10);
     if (const char* e = getenv("MINEHIP_LAUNCH_NONCES")) {
         const unsigned long long v = strtoull(e, nullptr, 10);
         if (v >= 1) o.max_nonces_per_launch = v;
@@ -402,6 +404,7 @@ int64_t mh_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, 
             q.word = p.J;
             q.mode = p.mode;
             q.blocks = p.blocks;
+            q.nonce_ops = p.ops;
         }
         ++k;
         return true;

@@ -110,6 +110,36 @@ void make_gen_args(const Prefix& pre, GenArgs* ga) {
     ga->t = pre.t;
 }
 
+uint32_t nonce_ops(int J, int mode) {
+    // nonce-level words: those depending on word J (same rule as the kernel)
+    uint64_t dep = 1ull << J;
+    for (int t = 16; t < 64; ++t)
+        if (((dep >> (t - 2)) | (dep >> (t - 7)) | (dep >> (t - 15)) | (dep >> (t - 16))) & 1ull) dep |= 1ull << t;
+    auto is = [&](int t) { return (dep >> t) & 1ull; };
+    uint32_t ops = 0;
+    for (int t = 16; t < 64; ++t) {
+        if (!is(t)) continue;
+        // sigma: 2 alignbit + shift + xor3; the sum of n terms takes ceil((n-1)/2) add3
+        const int s0 = (int)is(t - 15), s1 = (int)is(t - 2), a16 = (int)is(t - 16), a7 = (int)is(t - 7);
+        const int hoisted = (s0 && s1 && a16 && a7) ? 0 : 1;  // group/run-level partial sum
+        const int terms = s0 + s1 + a16 + a7 + hoisted;
+        ops += 4u * (uint32_t)(s0 + s1) + (uint32_t)(terms - 1 + 1) / 2u;
+    }
+    // round J: T1 = hoisted + digit, e' and a' one add each
+    ops += 3u;
+    // rounds J+1..63: 3+3 rotations, 2 xor3, Ch, Maj, 2 add3 for T1, e' add, a' add3 = 14;
+    // rounds J+1..J+3 read an invariant h and W, so h+K+W is hoisted (13)
+    for (int t = J + 1; t < 64; ++t) ops += (t <= J + 3 && !is(t)) ? 13u : 14u;
+    if (mode == kModeTwo) {
+        ops += 8u;                // feed-forward into block 1
+        ops += 64u * 14u - 1u;    // block 1 (its schedule is host-known); no e' in its last round
+    } else {
+        ops -= 1u;                // last round: e' is dead
+    }
+    ops += 3u;                    // last digit into W[J], H0 = st0 + a, compare
+    return ops;
+}
+
 namespace {
 
 // Fast-kernel launch template for bucket d with L lower digits.
@@ -197,6 +227,10 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const uint64_t B = std::min<uint64_t>(upper, d == 20 ? ~(uint64_t)0 : kPow10[d] - 1u);
         int L = std::min(opt.lower_digits, d - 1);
         L = std::min(L, 5);
+        // A lane runs 10^L nonces serially: a bucket with few runs would leave
+        // most SIMDs idle and take one lane's latency, so shorten the runs
+        // until the bucket fills the GPU (min_lanes ~ 4 waves on every SIMD).
+        while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
         FastArgs fa;
         int J = 0, mode = 0, nb = 1;
         while (L >= 1 && !make_fast_args(pre, d, L, &J, &mode, &nb, &fa)) --L;
@@ -231,6 +265,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             p.mode = mode;
             p.blocks = nb;
             p.fa = fa;
+            p.ops = nonce_ops(J, mode);
             p.fa.u_start = (uint64_t)u;
             p.fa.n_runs = (uint32_t)runs;
             p.ga = gbase;

@@ -40,12 +40,14 @@ struct Piece {
     int J;            // fast only
     int mode;         // fast only: FastMode
     int blocks;       // tail blocks of the final message
+    uint32_t ops;     // fast only: nonce_ops(J, mode)
     FastArgs fa;      // kind 0
     GenArgs ga;       // both (generic launch args; also used by hash_batch)
 };
 
 struct PlanOpts {
-    int lower_digits = 3;                        // L target
+    int lower_digits = 3;                        // L upper bound (nonces per lane = 10^L)
+    uint64_t min_lanes = 1u << 18;               // lower L until a bucket has this many runs
     uint64_t max_nonces_per_launch = 1ull << 32; // bounds one launch to ~0.1 s
 };
 
@@ -56,6 +58,12 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
 
 // Generic-kernel arguments for this prefix (first/count left 0).
 void make_gen_args(const Prefix& pre, GenArgs* ga);
+
+// Algorithmic VALU instructions per nonce of a fast piece: the SHA-256 work
+// that depends on the nonce's last digit (word J), with gfx950's 3-input ops
+// (14 per round, 4 per sigma, add3 sums); work shared by a group or a run is
+// amortised like the host midstate of SURVEY.md §8(d).  DESIGN.md §4.
+uint32_t nonce_ops(int J, int mode);
 
 int decimal_digits(uint64_t n);
 

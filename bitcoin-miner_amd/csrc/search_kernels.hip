@@ -20,9 +20,15 @@
 // Every candidate comparison is the lexicographic (hash, nonce) order, which
 // equals the reference loop's strict-< first minimum.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "layout.hpp"
 #include "sha256_gfx950.hpp"
+
+// minimum waves per SIMD the fast kernel is compiled for (register budget)
+#ifndef MH_MIN_WAVES
+#define MH_MIN_WAVES 1
+#endif
 
 namespace mh {
 namespace dev {
@@ -133,49 +139,64 @@ __device__ __forceinline__ void hash_generic(const GenArgs& a, uint64_t n, uint3
 }  // namespace dev
 
 // ---------------------------------------------------------------------------
-// fast_search<J, TWO>
+// fast_search<J, MODE>
 // ---------------------------------------------------------------------------
-// Which message-schedule words depend on word J (the only word that changes
-// from one nonce to the next inside a lane).  Bit t set <=> W[t] is
-// per-nonce.  Everything else is computed once per group (or per run) --
-// explicit hoisting: leaving it to LICM does not work because SROA turns the
-// message array into a loop-carried vector.
-template <int J>
-struct DepJ {
-    static constexpr uint64_t make() {
-        uint64_t m = 1ull << J;
+// Inside a lane only message word J (the last digit's word) changes from one
+// nonce to the next, and word J-1 changes once per group of 10 nonces.  Every
+// schedule word W[t] therefore lives at one of three levels, fixed at compile
+// time by J:
+//   nonce  depends on W[J]                    -> computed per nonce
+//   group  depends on W[J-1] but not on W[J]  -> once per 10 nonces
+//   run    neither                            -> once per lane (10^L nonces)
+// and each per-nonce / per-group word is split into its cheaper-level partial
+// sum plus the terms of its own level.  Words after J hold only padding and
+// length, so they come from the kernel arguments (SGPRs), never VGPRs.
+// The hoisting is explicit: left to LICM it does not happen, because SROA
+// turns the message array into a loop-carried vector.
+struct Dep {
+    static constexpr uint64_t from(int j) {  // words whose value depends on word j
+        if (j < 0) return 0;
+        uint64_t m = 1ull << j;
         for (int t = 16; t < 64; ++t)
             if (((m >> (t - 2)) | (m >> (t - 7)) | (m >> (t - 15)) | (m >> (t - 16))) & 1ull) m |= 1ull << t;
         return m;
     }
-    static constexpr uint64_t kMask = make();
 };
 
 namespace dev {
+// One round; kw = K[t] + W[t].  (h + kw) first, so it folds into a single
+// hoisted value whenever both are invariant.
 __device__ __forceinline__ void round_kw(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
                                          uint32_t& f, uint32_t& g, uint32_t& h, uint32_t kw) {
-    const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+    const uint32_t t1 = (h + kw) + bsig1(e) + ch(e, f, g);
     const uint32_t t2 = bsig0(a) + maj(a, b, c);
     h = g; g = f; f = e; e = d + t1;
     d = c; c = b; b = a; a = t1 + t2;
 }
 }  // namespace dev
 
-template <int J, bool TWO>
-__global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, Partial* __restrict__ partials) {
+template <int J, int MODE>
+__global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const FastArgs a,
+                                                                           Partial* __restrict__ partials) {
     using namespace dev;
     constexpr uint32_t K[64] = MH_K256;
-    constexpr uint64_t DEP = DepJ<J>::kMask;
-#define MH_DEP(t) ((DEP >> (t)) & 1ull)
+    constexpr uint64_t NM = Dep::from(J);               // nonce-level words
+    constexpr uint64_t GM = Dep::from(J - 1) & ~NM;     // group-level words
+    constexpr int BASE = (MODE == kModePre) ? 16 : 0;   // per-nonce block inside the tail
+#define MH_N(t) ((NM >> (t)) & 1ull)
+#define MH_G(t) ((GM >> (t)) & 1ull)
+#define MH_R(t) (!MH_N(t) && !MH_G(t))
     const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
     const uint64_t U = a.u_start + gid;
 
     // ---- per run --------------------------------------------------------
     // Tail words: host template + the d-L digits of U, right-aligned so U's
-    // last digit sits at tail byte hi_end-1.
-    uint32_t w[32];
+    // last digit sits at tail byte hi_end-1.  Only words before the lower
+    // digits can receive them (words < BASE + J).
+    constexpr int NW = BASE + J + 1;
+    uint32_t w[NW];
 #pragma unroll
-    for (int x = 0; x < 32; ++x) w[x] = a.blk[x];
+    for (int x = 0; x < NW; ++x) w[x] = a.blk[x];
     {
         uint64_t u = U;
 #pragma unroll
@@ -189,22 +210,38 @@ __global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, P
             }
         }
     }
+    // words of the per-nonce block: per-lane up to J, uniform (SGPR) after J
+    uint32_t W[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) W[t] = (t <= J) ? w[BASE + t] : a.blk[BASE + t];
+
     uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) st[i] = a.mid[i];
-    uint32_t wb[16];
-    if (!TWO && a.mode == kModePre) {
-        sha256_block(st, w);  // tail block 0 holds no lower digit: once per run
+    if constexpr (MODE == kModePre) {
+        uint32_t b0[16];
 #pragma unroll
-        for (int x = 0; x < 16; ++x) wb[x] = w[16 + x];
-    } else {
-#pragma unroll
-        for (int x = 0; x < 16; ++x) wb[x] = w[x];
+        for (int t = 0; t < 16; ++t) b0[t] = w[t];
+        sha256_block(st, b0);  // tail block 0 holds no lower digit: once per run
     }
     // rounds 0..J-2 read only run-level words
     uint32_t ra = st[0], rb = st[1], rc = st[2], rd = st[3], re = st[4], rf = st[5], rg = st[6], rh = st[7];
 #pragma unroll
-    for (int t = 0; t + 1 < J; ++t) round_kw(ra, rb, rc, rd, re, rf, rg, rh, K[t] + wb[t]);
+    for (int t = 0; t + 1 < J; ++t) round_kw(ra, rb, rc, rd, re, rf, rg, rh, K[t] + W[t]);
+
+    // run-level schedule words, and the run-level part of the others
+    uint32_t wr[64], pr[64];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) wr[t] = W[t];
+#pragma unroll
+    for (int t = 16; t < 64; ++t) {
+        uint32_t v = 0u;
+        if (MH_R(t - 16)) v += wr[t - 16];
+        if (MH_R(t - 7)) v += wr[t - 7];
+        if (MH_R(t - 15)) v += ssig0(wr[t - 15]);
+        if (MH_R(t - 2)) v += ssig1(wr[t - 2]);
+        if (MH_R(t)) wr[t] = v; else pr[t] = v;
+    }
 
     const uint32_t lastpos = a.lo_pos + a.L - 1u;  // byte of the last digit, in word J
     const uint32_t sh_last = 24u - 8u * (lastpos & 3u);
@@ -213,11 +250,11 @@ __global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, P
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
         // digits 0..L-2 of q = 10*g + i: wave-uniform, so this is SALU work
-        uint32_t cj = 0u, cjm = 0u, gg = g;
+        uint32_t cj = 0u, cjm = 0u, gq = g;
         for (uint32_t k = a.L - 1u; k-- > 0u;) {
-            const uint32_t q = gg / 10u;
-            const uint32_t dg = gg - q * 10u;
-            gg = q;
+            const uint32_t q = gq / 10u;
+            const uint32_t dg = gq - q * 10u;
+            gq = q;
             const uint32_t p = a.lo_pos + k;
             const uint32_t v = dg << (24u - 8u * (p & 3u));
             if ((p >> 2) == (uint32_t)J)
@@ -225,48 +262,48 @@ __global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, P
             else
                 cjm += v;
         }
-        const uint32_t wJ = wb[J] + cj;
-        uint32_t wi[64];  // group-level schedule words (valid where !DEP)
-        uint32_t pi[64];  // group-level part of the per-nonce words
-#pragma unroll
-        for (int t = 0; t < 16; ++t) wi[t] = (t == J - 1) ? wb[t] + cjm : wb[t];
+        const uint32_t wJ = W[J] + cj;  // word J with this group's digits, last digit '0'
+        uint32_t wg[64], pg[64];
+        if constexpr (J > 0) wg[J - 1] = W[J - 1] + cjm;
 #pragma unroll
         for (int t = 16; t < 64; ++t) {
-            if (!MH_DEP(t)) {
-                wi[t] = (wi[t - 16] + wi[t - 7]) + ssig0(wi[t - 15]) + ssig1(wi[t - 2]);
-            } else {
-                uint32_t v = 0u;
-                if (!MH_DEP(t - 16)) v += wi[t - 16];
-                if (!MH_DEP(t - 7)) v += wi[t - 7];
-                if (!MH_DEP(t - 15)) v += ssig0(wi[t - 15]);
-                if (!MH_DEP(t - 2)) v += ssig1(wi[t - 2]);
-                pi[t] = v;
-            }
+            if (MH_R(t)) continue;
+            uint32_t v = pr[t];
+            if (MH_G(t - 16)) v += wg[t - 16];
+            if (MH_G(t - 7)) v += wg[t - 7];
+            if (MH_G(t - 15)) v += ssig0(wg[t - 15]);
+            if (MH_G(t - 2)) v += ssig1(wg[t - 2]);
+            if (MH_G(t)) wg[t] = v; else pg[t] = v;
         }
         // round J-1 reads the group-level word J-1
-        uint32_t ga = ra, gb = rb, gc = rc, gd = rd, ge = re, gf = rf, gg2 = rg, gh = rh;
-        if constexpr (J > 0) round_kw(ga, gb, gc, gd, ge, gf, gg2, gh, K[J - 1] + wi[J - 1]);
+        uint32_t ga = ra, gb = rb, gc = rc, gd = rd, ge = re, gf = rf, gG = rg, gh = rh;
+        if constexpr (J > 0) round_kw(ga, gb, gc, gd, ge, gf, gG, gh, K[J - 1] + wg[J - 1]);
+        // round J: every input but W[J]'s last digit is known here
+        const uint32_t t1J = (gh + (K[J] + wJ)) + bsig1(ge) + ch(ge, gf, gG);
+        const uint32_t t2J = bsig0(ga) + maj(ga, gb, gc);
 
         for (uint32_t i = 0; i < 10u; ++i) {
             // ---- per nonce ------------------------------------------------
+            const uint32_t inc = i << sh_last;  // SALU
             uint32_t x[64];
-            x[J] = wJ + (i << sh_last);
+            x[J] = wJ + inc;
 #pragma unroll
             for (int t = 16; t < 64; ++t) {
-                if (MH_DEP(t)) {
-                    uint32_t v = pi[t];
-                    if (MH_DEP(t - 16)) v += x[t - 16];
-                    if (MH_DEP(t - 7)) v += x[t - 7];
-                    if (MH_DEP(t - 15)) v += ssig0(x[t - 15]);
-                    if (MH_DEP(t - 2)) v += ssig1(x[t - 2]);
-                    x[t] = v;
-                }
+                if (!MH_N(t)) continue;
+                uint32_t v = pg[t];
+                if (MH_N(t - 16)) v += x[t - 16];
+                if (MH_N(t - 7)) v += x[t - 7];
+                if (MH_N(t - 15)) v += ssig0(x[t - 15]);
+                if (MH_N(t - 2)) v += ssig1(x[t - 2]);
+                x[t] = v;
             }
-            uint32_t A = ga, B = gb, C = gc, D = gd, E = ge, F = gf, G = gg2, H = gh;
+            const uint32_t t1 = t1J + inc;
+            uint32_t A = t1 + t2J, B = ga, C = gb, D = gc, E = gd + t1, F = ge, G = gf, H = gG;
 #pragma unroll
-            for (int t = J; t < 64; ++t) round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_DEP(t) ? x[t] : wi[t]));
+            for (int t = J + 1; t < 64; ++t)
+                round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
             uint32_t h0, h1;
-            if constexpr (!TWO) {
+            if constexpr (MODE != kModeTwo) {
                 h0 = st[0] + A;
                 h1 = st[1] + B;
             } else {
@@ -283,7 +320,9 @@ __global__ __launch_bounds__(kBlockThreads) void fast_search(const FastArgs a, P
             }
         }
     }
-#undef MH_DEP
+#undef MH_N
+#undef MH_G
+#undef MH_R
 
     uint64_t hash = ((uint64_t)bh0 << 32) | bh1;
     uint64_t nonce = U * a.pow10L + bq;
@@ -340,31 +379,48 @@ __global__ __launch_bounds__(kBlockThreads) void merge_partials(const Partial* _
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
-template <int J, bool TWO>
+template <int J, int MODE>
 static hipError_t launch_fast_t(const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
-    hipLaunchKernelGGL((fast_search<J, TWO>), dim3(blocks), dim3(kBlockThreads), 0, s, a, partials);
+    // MINEHIP_DEV_LDS (experiments only): reserve dynamic LDS per workgroup to
+    // cap occupancy, e.g. 54000 -> 3 workgroups (waves/SIMD) per CU.
+    static const unsigned lds = [] {
+        const char* e = getenv("MINEHIP_DEV_LDS");
+        return e ? (unsigned)atoi(e) : 0u;
+    }();
+    hipLaunchKernelGGL((fast_search<J, MODE>), dim3(blocks), dim3(kBlockThreads), lds, s, a, partials);
     return hipGetLastError();
 }
 
-hipError_t launch_fast(int J, bool two, const FastArgs& a, Partial* partials,
-                       uint32_t blocks, hipStream_t s) {
-    if (!two) {
+hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
+#define MH_CASE(j, m) \
+    case j:           \
+        return launch_fast_t<j, m>(a, partials, blocks, s);
+    if (mode == kModeOne) {
         switch (J) {
-#define MH_CASE(j) \
-    case j:        \
-        return launch_fast_t<j, false>(a, partials, blocks, s);
-            MH_CASE(0) MH_CASE(1) MH_CASE(2) MH_CASE(3) MH_CASE(4) MH_CASE(5) MH_CASE(6)
-            MH_CASE(7) MH_CASE(8) MH_CASE(9) MH_CASE(10) MH_CASE(11) MH_CASE(12) MH_CASE(13)
-#undef MH_CASE
+            MH_CASE(0, kModeOne) MH_CASE(1, kModeOne) MH_CASE(2, kModeOne) MH_CASE(3, kModeOne)
+            MH_CASE(4, kModeOne) MH_CASE(5, kModeOne) MH_CASE(6, kModeOne) MH_CASE(7, kModeOne)
+            MH_CASE(8, kModeOne) MH_CASE(9, kModeOne) MH_CASE(10, kModeOne) MH_CASE(11, kModeOne)
+            MH_CASE(12, kModeOne) MH_CASE(13, kModeOne)
             default: return hipErrorInvalidValue;
         }
     }
-    switch (J) {
-        case 13: return launch_fast_t<13, true>(a, partials, blocks, s);
-        case 14: return launch_fast_t<14, true>(a, partials, blocks, s);
-        case 15: return launch_fast_t<15, true>(a, partials, blocks, s);
-        default: return hipErrorInvalidValue;
+    if (mode == kModePre) {
+        switch (J) {
+            MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
+            MH_CASE(4, kModePre) MH_CASE(5, kModePre) MH_CASE(6, kModePre) MH_CASE(7, kModePre)
+            MH_CASE(8, kModePre) MH_CASE(9, kModePre) MH_CASE(10, kModePre) MH_CASE(11, kModePre)
+            MH_CASE(12, kModePre) MH_CASE(13, kModePre)
+            default: return hipErrorInvalidValue;
+        }
     }
+    if (mode == kModeTwo) {
+        switch (J) {
+            MH_CASE(13, kModeTwo) MH_CASE(14, kModeTwo) MH_CASE(15, kModeTwo)
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef MH_CASE
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {

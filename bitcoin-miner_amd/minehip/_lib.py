@@ -29,7 +29,7 @@ EXPORTS = (
 class mh_piece(ctypes.Structure):
     _fields_ = [("first", ctypes.c_uint64), ("count", ctypes.c_uint64), ("kind", ctypes.c_int32),
                 ("digits", ctypes.c_int32), ("lo_digits", ctypes.c_int32), ("word", ctypes.c_int32),
-                ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32)]
+                ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32), ("nonce_ops", ctypes.c_uint32)]
 
 
 class mh_message(ctypes.Structure):

@@ -126,14 +126,16 @@ int mh_profile_enable(int dev, int on);
  *   out[0] launches of the dominant (fast search) kernel
  *   out[1] nonces those launches processed
  *   out[2] summed kernel duration, nanoseconds (HIP events on the lib's stream)
- *   out[3] algorithmic VALU ops of those launches
- *          (MH_OPS_PER_BLOCK x per-nonce SHA-256 compressions)
+ *   out[3] algorithmic VALU instructions of those launches: per piece,
+ *          nonces x mh_piece.nonce_ops (the nonce-dependent SHA-256 work,
+ *          DESIGN.md §4); x64 lanes = int32 lane-ops
  *   out[4] nonces processed by the generic (edge) kernel
  *   out[5] generic kernel duration, nanoseconds
  * n = number of slots the caller provides (<= 8). */
 int mh_profile_read(int dev, uint64_t *out, int n);
 
-/* Canonical gfx950 VALU ops for one SHA-256 compression. */
+/* gfx950 VALU instructions of one full SHA-256 compression with no work
+ * hoisted (64 rounds x 14 + 48 schedule words x 10). */
 #define MH_OPS_PER_BLOCK 1376u
 
 /* ---- introspection (host only, no GPU needed; used by CPU tests) -------- */
@@ -148,6 +150,7 @@ typedef struct mh_piece {
     int32_t word;       /* fast: message word holding the last digit (J)   */
     int32_t mode;       /* fast: 0 one block, 1 prefix block per run, 2 two blocks per nonce */
     int32_t blocks;     /* tail blocks hashed per nonce in the final message */
+    uint32_t nonce_ops; /* fast: algorithmic VALU instructions per nonce */
 } mh_piece;
 
 /* Plan the search of [lower, upper] for `msg`: writes the pieces in

@@ -117,7 +117,7 @@ def test_plan_invariance_small(gpu):
                       (b"a" * 100, 123, 345_678), (b"y" * 52, 10 ** 12 - 50_000, 10 ** 12 + 50_000)):
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 2, 3, 4, 5):
-            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_LAUNCH_NONCES=100_000):
+            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000):
                 assert gpu.search(m, lo, hi) == exp, (m[:8], Ld)
 
 
@@ -132,9 +132,9 @@ def test_full_size_properties(gpu, msg, bits):
     for _ in range(2):  # split-range associativity
         mid = rng.randrange(1, hi)
         assert lexmin(gpu.search(msg, 0, mid), gpu.search(msg, mid + 1, hi)) == r
-    with env(MINEHIP_LOWER_DIGITS=4):
+    with env(MINEHIP_LOWER_DIGITS=4, MINEHIP_MIN_LANES=1):
         assert gpu.search(msg, 0, hi) == r
-    with env(MINEHIP_LOWER_DIGITS=2, MINEHIP_LAUNCH_NONCES=1 << 28):
+    with env(MINEHIP_LOWER_DIGITS=1, MINEHIP_LAUNCH_NONCES=1 << 28):
         assert gpu.search(msg, 0, hi) == r
     assert gpu.search_multi(msg, 0, hi, devs=[0, 0, 0], chunk=(1 << bits) // 7 + 3) == r
     # no sampled nonce beats it (oracle on 200k random nonces of the range)

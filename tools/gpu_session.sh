@@ -63,6 +63,22 @@ for s in $STEPS; do
           -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc3.err")
       rc=$?; echo "pmc3 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       ;;
+    valu)
+      timeout -k 10 120 "$ROOT/build/valu_peak" > "$OUT/valu_peak.json" 2>&1
+      rc=$?; echo "valu rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_peak.json"; fatal $rc
+      ;;
+    valuops)
+      timeout -k 10 300 "$ROOT/build/valu_ops" > "$OUT/valu_ops.json" 2>&1
+      rc=$?; echo "valuops rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_ops.json"; fatal $rc
+      ;;
+    valumix)
+      timeout -k 10 300 "$ROOT/build/valu_mix" > "$OUT/valu_mix.json" 2>&1
+      rc=$?; echo "valumix rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_mix.json"; fatal $rc
+      ;;
+    kbench)
+      timeout -k 10 600 python "$ROOT/tools/kbench.py" ${KBENCH_ARGS:-} > "$OUT/kbench.json" 2> "$OUT/kbench.err"
+      rc=$?; echo "kbench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/kbench.json"; tail -3 "$OUT/kbench.err"; fatal $rc
+      ;;
     *) echo "unknown step $s";;
   esac
 done

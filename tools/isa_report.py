@@ -1,0 +1,81 @@
+"""Per-kernel register use and per-nonce issue cost from the gfx950 assembly.
+
+  make asm && python tools/isa_report.py build/search_kernels.s [filter]
+
+For every kernel: VGPRs/SGPRs/scratch from the metadata, and for the
+innermost loop (the per-nonce body of fast_search) the VALU instruction count,
+split into full-rate (1 issue slot) and half-rate (2 slots) instructions as
+measured by tools/valu_ops.hip on MI355X.
+"""
+import re
+import sys
+from collections import Counter
+
+# measured on MI355X (tools/valu_ops.hip): ~63 lanes/clk/CU instead of ~120
+HALF_RATE = {
+    "v_alignbit_b32", "v_alignbyte_b32", "v_add3_u32", "v_xad_u32", "v_bfi_b32", "v_lshl_or_b32",
+    "v_lshl_add_u32", "v_and_or_b32", "v_or3_b32", "v_perm_b32", "v_cndmask_b32_e64", "v_mad_u32_u24",
+    "v_lshrrev_b64", "v_lshlrev_b64", "v_mov_b64", "v_lshlrev_b32_e64", "v_lshrrev_b32_e64",
+    "v_mad_u64_u32", "v_pk_add_u16",
+}
+
+
+def kernels(text):
+    out = {}
+    for m in re.finditer(r"^(_Z\S+):", text, flags=re.M):
+        name = m.group(1)
+        end = text.find("s_endpgm", m.end())
+        out[name] = text[m.end():end]
+    return out
+
+
+def meta(text):
+    res = {}
+    for blk in re.finditer(r"\.name:\s+(_Z\S+)(.*?)(?=\n\s+- \.|\Z)", text, flags=re.S):
+        d = {}
+        for k in ("vgpr_count", "sgpr_count", "private_segment_fixed_size", "vgpr_spill_count"):
+            mm = re.search(r"\." + k + r":\s+(\d+)", blk.group(2))
+            if mm:
+                d[k] = int(mm.group(1))
+        res[blk.group(1)] = d
+    return res
+
+
+def inner_loop(body):
+    lines = body.split("\n")
+    best = None
+    for i, l in enumerate(lines):
+        if "Inner Loop Header" in l or ("Loop Header: Depth=1" in l and best is None):
+            ins = []
+            for j in range(i, len(lines)):
+                s = lines[j].strip()
+                if s.startswith("v_"):
+                    ins.append(s.split()[0])
+                if s.startswith("s_cbranch_scc") or s.startswith("s_branch"):
+                    break
+            if best is None or len(ins) > len(best):
+                best = ins
+    return best or []
+
+
+def main():
+    path = sys.argv[1]
+    filt = sys.argv[2] if len(sys.argv) > 2 else ""
+    text = open(path).read()
+    md = meta(text)
+    for name, body in kernels(text).items():
+        if filt not in name:
+            continue
+        ins = inner_loop(body)
+        c = Counter(ins)
+        half = sum(v for k, v in c.items() if k in HALF_RATE)
+        full = len(ins) - half
+        m = md.get(name, {})
+        short = re.sub(r"EvNS_8FastArgsEPNS_7PartialE$", "", name)
+        print(f"{short:40s} vgpr={m.get('vgpr_count')} sgpr={m.get('sgpr_count')} "
+              f"scratch={m.get('private_segment_fixed_size')} loop_valu={len(ins)} half={half} full={full} "
+              f"slots={2 * half + full}  top={c.most_common(5)}")
+
+
+if __name__ == "__main__":
+    main()

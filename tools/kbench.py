@@ -1,0 +1,55 @@
+"""Kernel-level A/B bench: GH/s of the fast kernel on one decimal bucket
+(HIP-event time from the library's profile counters), interleaving
+configurations given as env settings inside ONE process.
+
+  python tools/kbench.py --msg cmu440 --lo 1000000000 --count 2147483648 \
+      --var base: --var lds3:MINEHIP_DEV_LDS=54000 --rounds 3
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
+import minehip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--msg", default="cmu440")
+    ap.add_argument("--lo", type=int, default=10 ** 9)
+    ap.add_argument("--count", type=int, default=1 << 31)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--var", action="append", default=[], help="name:K=V,K=V")
+    a = ap.parse_args()
+    variants = []
+    for v in a.var or ["base:"]:
+        name, _, kv = v.partition(":")
+        env = dict(x.split("=", 1) for x in kv.split(",") if x)
+        variants.append((name, env))
+    res = {n: [] for n, _ in variants}
+    minehip.search(a.msg, a.lo, a.lo + (1 << 26))  # warm up / load code objects
+    for _ in range(a.rounds):
+        for name, env in variants:
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            minehip.profile_enable(0, True)
+            r = minehip.search(a.msg, a.lo, a.lo + a.count - 1)
+            p = minehip.profile_read(0)
+            minehip.profile_enable(0, False)
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            ns = p["fast_ns"] + p["generic_ns"]
+            res[name].append({"ghs": a.count / ns, "fast_ghs": p["fast_nonces"] / max(1, p["fast_ns"]),
+                              "result": r})
+    out = {n: {"ghs_max": max(x["ghs"] for x in v), "ghs_med": sorted(x["ghs"] for x in v)[len(v) // 2],
+               "fast_ghs_max": max(x["fast_ghs"] for x in v), "result": v[-1]["result"]} for n, v in res.items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
