@@ -162,6 +162,8 @@ def test_profile_counters(gpu):
     gpu.search("cmu440", 0, (1 << 30) - 1)
     p = gpu.profile_read(0)
     gpu.profile_enable(0, False)
-    assert p["fast_launches"] >= 1 and p["fast_ns"] > 0
+    plan = gpu.plan("cmu440", 0, (1 << 30) - 1)
+    fast = [q for q in plan if q["kind"] == 0]
+    assert p["fast_launches"] == len(fast) and p["fast_ns"] > 0
     assert p["fast_nonces"] + p["generic_nonces"] == 1 << 30
-    assert p["fast_ops"] == p["fast_nonces"] * 1376
+    assert p["fast_ops"] == sum(q["count"] * q["nonce_ops"] for q in fast)
