@@ -164,7 +164,8 @@ bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, 
     const uint32_t lo = pl - (uint32_t)L + 1u - base;  // first lower digit, per-nonce-block relative
     const int J = (int)((pl - base) >> 2);
     if ((int)(lo >> 2) < J - 1) return false;  // lower digits must span words J-1..J only
-    if (mode == kModeTwo ? (J < 13 || J > 15) : (J < 0 || J > 13)) return false;
+    // the instantiated kernels (search_kernels.hip launch_fast)
+    if (mode == kModeTwo ? (J < 13 || J > 15) : (J < 0 || J > (mode == kModePre ? 4 : 13))) return false;
 
     memset(fa, 0, sizeof *fa);
     memcpy(fa->mid, pre.mid, sizeof pre.mid);

@@ -404,12 +404,10 @@ hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, ui
             default: return hipErrorInvalidValue;
         }
     }
-    if (mode == kModePre) {
+    if (mode == kModePre) {  // last digit at tail byte 64..82 (t <= 63, d <= 20): J <= 4
         switch (J) {
             MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
-            MH_CASE(4, kModePre) MH_CASE(5, kModePre) MH_CASE(6, kModePre) MH_CASE(7, kModePre)
-            MH_CASE(8, kModePre) MH_CASE(9, kModePre) MH_CASE(10, kModePre) MH_CASE(11, kModePre)
-            MH_CASE(12, kModePre) MH_CASE(13, kModePre)
+            MH_CASE(4, kModePre)
             default: return hipErrorInvalidValue;
         }
     }

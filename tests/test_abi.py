@@ -182,3 +182,24 @@ def test_miner_handle_rejects_non_requests():
     with pytest.raises(minehip.MinehipError) as e:
         minehip.miner_handle(minehip.marshal(minehip.NewRequest("x", 9, 1)))
     assert e.value.code == minehip.MH_ERANGE
+
+
+KERNELS = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(13, 2), (14, 2), (15, 2)}
+
+
+def kernel_cases():
+    """One (msg, lo, hi) per instantiated fast kernel (word J, mode)."""
+    seen = {}
+    for L in range(0, 128):
+        m = b"q" * L
+        for d in range(2, 21):
+            lo = 10 ** (d - 1)
+            hi = min(U64, lo + 5000)
+            for p in minehip.plan(m, lo, hi):
+                if p["kind"] == 0:
+                    seen.setdefault((p["word"], p["mode"]), (m, lo, hi))
+    return seen
+
+
+def test_every_instantiated_kernel_is_reachable():
+    assert set(kernel_cases()) == KERNELS

@@ -61,3 +61,12 @@ def test_sharded_merge_matches_full_scan(world):
 def test_merge_is_lexicographic():
     assert bench.merge([(5, 9), (5, 3), (7, 1)]) == (5, 3)
     assert bench.shard(3, 32) == (3 << 32, (4 << 32) - 1)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_rank_ranges_tile_the_space(world):
+    for bits, scaling in ((32, "weak"), (40, "strong"), (7, "strong")):
+        rs = [bench.rank_range(r, world, bits, scaling) for r in range(world)]
+        assert rs[0][0] == 0 and all(rs[i][1] + 1 == rs[i + 1][0] for i in range(world - 1))
+        total = (1 << bits) * (world if scaling == "weak" else 1)
+        assert rs[-1][1] == total - 1

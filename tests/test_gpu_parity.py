@@ -97,6 +97,21 @@ def test_every_tail_offset_and_bucket(gpu):
             assert gpu.search(m, lo, hi) == oracle.search(m, lo, hi, threads=8), (L, lo, hi)
 
 
+def test_every_kernel_instantiation(gpu):
+    """Each of the 22 fast_search<J, MODE> kernels, at the shortest and the
+    longest lane runs (L = 1 and the largest L the layout allows), bit-exact
+    against the oracle over ranges holding whole runs plus ragged edges."""
+    from test_abi import KERNELS, kernel_cases
+    cases = kernel_cases()
+    assert set(cases) == KERNELS
+    for (J, mode), (m, lo, _) in sorted(cases.items()):
+        hi = lo + 23_456
+        exp = oracle.search(m, lo, hi, threads=8)
+        for Ld in (1, 3):
+            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1):
+                assert gpu.search(m, lo, hi) == exp, (J, mode, len(m), Ld)
+
+
 def test_u64_edges(gpu):
     for m in (b"cmu440", b"", b"q" * 60, b"r" * 119):
         assert gpu.search(m, U64, U64) == (oracle.hash_(m, U64), U64)

@@ -79,6 +79,12 @@ for s in $STEPS; do
       timeout -k 10 600 python "$ROOT/tools/kbench.py" ${KBENCH_ARGS:-} > "$OUT/kbench.json" 2> "$OUT/kbench.err"
       rc=$?; echo "kbench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/kbench.json"; tail -3 "$OUT/kbench.err"; fatal $rc
       ;;
+    benchcfg)
+      for c in 3a 3b; do
+        timeout -k 10 600 python "$ROOT/bench.py" --config $c --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_cfg$c.json" 2> "$OUT/bench_cfg$c.err"
+        rc=$?; echo "bench cfg $c rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_cfg$c.json"; fatal $rc
+      done
+      ;;
     *) echo "unknown step $s";;
   esac
 done
