@@ -8,10 +8,21 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSRC)/message.cpp
 HDRS    := $(CSRC)/layout.hpp $(CSRC)/plan.hpp $(CSRC)/sha256_gfx950.hpp include/minehip.h
 
-all: $(LIB) oracle
+BIN     := $(PKG)/bin
+CLIS    := $(BIN)/minehip-search $(BIN)/minehip-miner
+
+all: $(LIB) $(CLIS) oracle
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+
+# native C++ callers of the C-ABI (rpath: the library next to the package)
+$(BIN)/minehip-search: $(CSRC)/cli.cpp include/minehip.h $(LIB)
+	mkdir -p $(BIN)
+	g++ -O2 -std=c++17 -Wall -o $@ $(CSRC)/cli.cpp -L$(PKG)/minehip -lminehip -Wl,-rpath,'$$ORIGIN/../minehip'
+
+$(BIN)/minehip-miner: $(BIN)/minehip-search
+	ln -sf minehip-search $@
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -22,7 +33,7 @@ asm: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
 clean:
-	rm -f $(LIB)
+	rm -f $(LIB) $(CLIS)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean
