@@ -277,9 +277,11 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     mh::absorb_prefix(msg, len, &pre);
     const uint64_t span = upper - lower;  // count - 1
     if (chunk == 0) {
-        // >= 8 chunks per device for dynamic balance, >= 2^32 nonces each
+        // ~8 chunks per device for dynamic balance (buckets differ in cost),
+        // but >= 2^30 nonces (~33 ms) each so the per-chunk launch and sync
+        // overhead (~0.1 ms) stays under 1%
         const uint64_t want = span / ((uint64_t)ndev * 8u) + 1u;
-        chunk = want < (1ull << 32) ? (1ull << 32) : want;
+        chunk = want < (1ull << 30) ? (1ull << 30) : want;
     }
     const uint64_t nchunks = span / chunk + 1u;  // chunk >= 1
     std::atomic<uint64_t> next{0};

@@ -85,6 +85,10 @@ for s in $STEPS; do
         rc=$?; echo "bench cfg $c rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_cfg$c.json"; fatal $rc
       done
       ;;
+    latency)
+      timeout -k 10 300 python "$ROOT/tools/latency.py" > "$OUT/latency.json" 2> "$OUT/latency.err"
+      rc=$?; echo "latency rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/latency.json"; fatal $rc
+      ;;
     *) echo "unknown step $s";;
   esac
 done
