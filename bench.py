@@ -141,6 +141,8 @@ def main():
     ap.add_argument("--msg", default=None, help="override the config's message")
     ap.add_argument("--bits", type=int, default=None, help="override log2 nonces per GPU (weak) / total (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="backend of the 16-byte merge and the timing max (nccl = RCCL on ROCm)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.msg is not None:
@@ -151,6 +153,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # test-only: run every rank on one device (rehearsing N>1 on a 1-GPU box; gloo only,
+    # RCCL refuses two ranks on one GPU)
+    if os.environ.get("BENCH_DEVICE") is not None:
+        local = int(os.environ["BENCH_DEVICE"])
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
@@ -158,9 +164,13 @@ def main():
     dist = None
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    comm_device = device if args.dist_backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import minehip
     if minehip.device_count() <= local:
@@ -174,13 +184,13 @@ def main():
     for _ in range(args.warmup):
         search(lo, hi)
     minehip.profile_enable(local, True)
-    r, elapsed = run_steps(search, lo, hi, args.steps, 0, world, dist, torch, device, torch.cuda.synchronize)
+    r, elapsed = run_steps(search, lo, hi, args.steps, 0, world, dist, torch, comm_device, torch.cuda.synchronize)
     prof = minehip.profile_read(local)
     minehip.profile_enable(local, False)
 
     t_max = elapsed
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
 

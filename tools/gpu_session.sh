@@ -89,6 +89,13 @@ for s in $STEPS; do
       timeout -k 10 300 python "$ROOT/tools/latency.py" > "$OUT/latency.json" 2> "$OUT/latency.err"
       rc=$?; echo "latency rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/latency.json"; fatal $rc
       ;;
+    dist2)
+      # 2 ranks on the box's one GPU over gloo: exercises bench.py's multi-process path
+      BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29533 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 \
+          --dist-backend gloo > "$OUT/dist2.json" 2> "$OUT/dist2.err"
+      rc=$?; echo "dist2 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist2.json"; fatal $rc
+      ;;
     *) echo "unknown step $s";;
   esac
 done
