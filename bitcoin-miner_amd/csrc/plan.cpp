@@ -123,7 +123,9 @@ uint32_t nonce_ops(int J, int mode) {
         const int s0 = (int)is(t - 15), s1 = (int)is(t - 2), a16 = (int)is(t - 16), a7 = (int)is(t - 7);
         const int hoisted = (s0 && s1 && a16 && a7) ? 0 : 1;  // group/run-level partial sum
         const int terms = s0 + s1 + a16 + a7 + hoisted;
-        ops += 4u * (uint32_t)(s0 + s1) + (uint32_t)(terms - 1 + 1) / 2u;
+        // sigma(W[J]) = sigma(wJ) ^ sigma(digit): one xor (the last digit never carries)
+        const uint32_t sig = (uint32_t)(s0 ? (t - 15 == J ? 1 : 4) : 0) + (uint32_t)(s1 ? (t - 2 == J ? 1 : 4) : 0);
+        ops += sig + (uint32_t)(terms - 1 + 1) / 2u;
     }
     // round J: T1 = hoisted + digit, e' and a' one add each
     ops += 3u;
@@ -136,7 +138,9 @@ uint32_t nonce_ops(int J, int mode) {
     } else {
         ops -= 1u;                // last round: e' is dead
     }
-    ops += 3u;                    // last digit into W[J], H0 = st0 + a, compare
+    // The last round's sum absorbs K[63] + st0, so H0 costs no extra add;
+    // H1 and the 64-bit compare run only on the rare new-best branch.
+    ops += 2u;                    // last digit into W[J], compare H0
     return ops;
 }
 

@@ -163,7 +163,39 @@ struct Dep {
     }
 };
 
+// sigma0/sigma1 of the last digit's contribution inc = i << 8k (i = 0..9,
+// k = byte slot).  The last digit's byte of word J is '0' before the digit
+// is added and 0x30 + i never carries, so W[J] = wJ ^ inc and, sigma being
+// GF(2)-linear, sigma(W[J]) = sigma(wJ) ^ sigma(inc): one VALU xor per nonce
+// with a scalar (SMEM) operand instead of four VALU ops.
+struct IncSigma {
+    uint32_t s0[4][10], s1[4][10];
+};
+constexpr uint32_t crotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+constexpr IncSigma make_inc_sigma() {
+    IncSigma t{};
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t i = 0; i < 10; ++i) {
+            const uint32_t x = i << (8 * k);
+            t.s0[k][i] = crotr(x, 7) ^ crotr(x, 18) ^ (x >> 3);
+            t.s1[k][i] = crotr(x, 17) ^ crotr(x, 19) ^ (x >> 10);
+        }
+    return t;
+}
+__constant__ IncSigma kIncSigma = make_inc_sigma();
+
 namespace dev {
+// Last round of a compression when only H0 = st0 + a64 is needed:
+// kw_st0 = K[63] + W[63] + st0.  Seven terms, three add3.
+__device__ __forceinline__ uint32_t last_round_h0(uint32_t a, uint32_t b, uint32_t c, uint32_t e, uint32_t f,
+                                                  uint32_t g, uint32_t h, uint32_t kw_st0) {
+    return ((h + kw_st0) + bsig1(e) + ch(e, f, g)) + (bsig0(a) + maj(a, b, c));
+}
+
+// Block whose schedule is host-known (kw[i] = K[i] + W[i]): H0 and a63.
+__device__ __forceinline__ void sha256_block_kw_last(const uint32_t st[8], const uint32_t* kw, uint32_t& h0,
+                                                     uint32_t& a63);
+
 // One round; kw = K[t] + W[t].  (h + kw) first, so it folds into a single
 // hoisted value whenever both are invariant.
 __device__ __forceinline__ void round_kw(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
@@ -172,6 +204,15 @@ __device__ __forceinline__ void round_kw(uint32_t& a, uint32_t& b, uint32_t& c, 
     const uint32_t t2 = bsig0(a) + maj(a, b, c);
     h = g; g = f; f = e; e = d + t1;
     d = c; c = b; b = a; a = t1 + t2;
+}
+
+__device__ __forceinline__ void sha256_block_kw_last(const uint32_t st[8], const uint32_t* kw, uint32_t& h0,
+                                                     uint32_t& a63) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int i = 0; i < 63; ++i) round_kw(a, b, c, d, e, f, g, h, kw[i]);
+    a63 = a;
+    h0 = last_round_h0(a, b, c, e, f, g, h, kw[63] + st[0]);
 }
 }  // namespace dev
 
@@ -263,6 +304,7 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
                 cjm += v;
         }
         const uint32_t wJ = W[J] + cj;  // word J with this group's digits, last digit '0'
+        const uint32_t s0wJ = ssig0(wJ), s1wJ = ssig1(wJ);
         uint32_t wg[64], pg[64];
         if constexpr (J > 0) wg[J - 1] = W[J - 1] + cjm;
 #pragma unroll
@@ -285,6 +327,7 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
         for (uint32_t i = 0; i < 10u; ++i) {
             // ---- per nonce ------------------------------------------------
             const uint32_t inc = i << sh_last;  // SALU
+            const uint32_t s0inc = kIncSigma.s0[sh_last >> 3][i], s1inc = kIncSigma.s1[sh_last >> 3][i];
             uint32_t x[64];
             x[J] = wJ + inc;
 #pragma unroll
@@ -293,25 +336,35 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
                 uint32_t v = pg[t];
                 if (MH_N(t - 16)) v += x[t - 16];
                 if (MH_N(t - 7)) v += x[t - 7];
-                if (MH_N(t - 15)) v += ssig0(x[t - 15]);
-                if (MH_N(t - 2)) v += ssig1(x[t - 2]);
+                if (MH_N(t - 15)) v += (t - 15 == J) ? (s0wJ ^ s0inc) : ssig0(x[t - 15]);
+                if (MH_N(t - 2)) v += (t - 2 == J) ? (s1wJ ^ s1inc) : ssig1(x[t - 2]);
                 x[t] = v;
             }
             const uint32_t t1 = t1J + inc;
             uint32_t A = t1 + t2J, B = ga, C = gb, D = gc, E = gd + t1, F = ge, G = gf, H = gG;
-#pragma unroll
-            for (int t = J + 1; t < 64; ++t)
-                round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
-            uint32_t h0, h1;
+            uint32_t h0, a63;
             if constexpr (MODE != kModeTwo) {
-                h0 = st[0] + A;
-                h1 = st[1] + B;
+#pragma unroll
+                for (int t = J + 1; t < 63; ++t)
+                    round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
+                a63 = A;
+                h0 = last_round_h0(A, B, C, E, F, G, H,
+                                   (K[63] + st[0]) + (MH_N(63) ? x[63] : (MH_G(63) ? wg[63] : wr[63])));
             } else {
-                uint32_t s2[8] = {st[0] + A, st[1] + B, st[2] + C, st[3] + D,
-                                  st[4] + E, st[5] + F, st[6] + G, st[7] + H};
-                sha256_block_kw_h01(s2, a.kw1, h0, h1);  // block 1: padding + length only
+#pragma unroll
+                for (int t = J + 1; t < 64; ++t)
+                    round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
+                const uint32_t s2[8] = {st[0] + A, st[1] + B, st[2] + C, st[3] + D,
+                                        st[4] + E, st[5] + F, st[6] + G, st[7] + H};
+                sha256_block_kw_last(s2, a.kw1, h0, a63);  // block 1: padding + length only
+                a63 += s2[1] - st[1];                       // so that H1 = st[1] + a63 below
             }
-            if (h0 <= bh0) {
+            // New best (rare after the first nonces): a real branch, not
+            // if-converted selects, so H1 and the 64-bit compare cost nothing
+            // on the common path.
+            if (__builtin_expect(h0 <= bh0, 0)) {
+                asm volatile("" ::);
+                const uint32_t h1 = st[1] + a63;
                 if (h0 < bh0 || h1 < bh1) {
                     bh0 = h0;
                     bh1 = h1;
