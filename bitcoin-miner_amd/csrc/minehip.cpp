@@ -60,7 +60,14 @@ constexpr int kEventPairs = 512;             // profiled launches buffered befor
 struct Timed {
     hipEvent_t start, stop;
     int kind;  // 0 fast, 1 generic
+    int var;   // fast: kernel variant index (J + 16 * mode)
 };
+
+// per fast_search<J, MODE> variant: launches, nonces, ns, algorithmic instructions
+struct VarStat {
+    uint64_t launches = 0, nonces = 0, ns = 0, ops = 0;
+};
+constexpr int kVariants = 48;  // J < 16, mode < 3
 
 struct DevCtx {
     std::mutex mu;
@@ -77,6 +84,7 @@ struct DevCtx {
     std::vector<Timed> pool;
     int used = 0;
     uint64_t cnt[8] = {0};
+    VarStat var[kVariants];
 };
 
 std::mutex g_tab_mu;
@@ -135,6 +143,7 @@ int harvest_locked(DevCtx* c) {
         MH_HIP(hipEventElapsedTime(&ms, c->pool[(size_t)i].start, c->pool[(size_t)i].stop));
         const uint64_t ns = (uint64_t)((double)ms * 1.0e6);
         c->cnt[c->pool[(size_t)i].kind == 0 ? 2 : 5] += ns;
+        if (c->pool[(size_t)i].kind == 0) c->var[c->pool[(size_t)i].var].ns += ns;
     }
     c->used = 0;
     return MH_OK;
@@ -151,6 +160,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
         }
         tm = &c->pool[(size_t)c->used++];
         tm->kind = p.kind;
+        tm->var = p.J + 16 * p.mode;
         MH_HIP(hipEventRecord(tm->start, c->stream));
     }
     uint32_t blocks;
@@ -175,6 +185,10 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
             c->cnt[0] += 1;
             c->cnt[1] += p.count;
             c->cnt[3] += p.count * (uint64_t)p.ops;
+            VarStat& v = c->var[p.J + 16 * p.mode];
+            v.launches += 1;
+            v.nonces += p.count;
+            v.ops += p.count * (uint64_t)p.ops;
         } else {
             c->cnt[4] += p.count;
         }
@@ -361,6 +375,7 @@ int mh_profile_enable(int dev, int on) {
     MH_HIP(hipStreamSynchronize(c->stream));
     c->used = 0;
     memset(c->cnt, 0, sizeof c->cnt);
+    for (auto& v : c->var) v = VarStat();
     c->prof = on != 0;
     return MH_OK;
 }
@@ -379,6 +394,35 @@ int mh_profile_read(int dev, uint64_t* out, int n) {
     }
     for (int i = 0; i < n && i < 8; ++i) out[i] = c->cnt[i];
     return MH_OK;
+}
+
+int mh_profile_kernels(int dev, mh_kernel_stat* out, int cap) {
+    g_err.clear();
+    if (cap < 0 || (!out && cap > 0)) return fail(MH_EINVAL, "bad arguments");
+    DevCtx* c;
+    int rc = get_ctx(dev, &c);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->ready) {
+        MH_HIP(hipStreamSynchronize(c->stream));
+        rc = harvest_locked(c);
+        if (rc) return rc;
+    }
+    int n = 0;
+    for (int i = 0; i < kVariants; ++i) {
+        const VarStat& v = c->var[i];
+        if (!v.launches) continue;
+        if (n < cap) {
+            out[n].word = i % 16;
+            out[n].mode = i / 16;
+            out[n].launches = v.launches;
+            out[n].nonces = v.nonces;
+            out[n].ns = v.ns;
+            out[n].ops = v.ops;
+        }
+        ++n;
+    }
+    return n;
 }
 
 int64_t mh_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, mh_piece* out, int64_t cap) {

@@ -17,7 +17,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import lib, mh_piece, mh_message, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
+from ._lib import lib, mh_piece, mh_message, mh_kernel_stat, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
 from ._lib import MH_OK, MH_EINVAL, MH_ERANGE, MH_ETOOLONG, MH_ENODEV, MH_EHIP  # noqa: F401
 
 U64_MAX = (1 << 64) - 1
@@ -97,6 +97,18 @@ def profile_read(dev=0):
     _check(lib.mh_profile_read(dev, out, 8))
     keys = ("fast_launches", "fast_nonces", "fast_ns", "fast_ops", "generic_nonces", "generic_ns")
     return {k: int(out[i]) for i, k in enumerate(keys)}
+
+
+def profile_kernels(dev=0):
+    """Per fast_search<J, MODE> variant: launches, nonces, ns, ops (largest ns first)."""
+    buf = (mh_kernel_stat * 64)()
+    n = lib.mh_profile_kernels(dev, buf, 64)
+    if n < 0:
+        _check(n)
+    out = [{f: int(getattr(buf[i], f)) for f, _ in mh_kernel_stat._fields_} for i in range(min(n, 64))]
+    for k in out:
+        k["name"] = f"mh::fast_search<{k['word']}, {k['mode']}>"
+    return sorted(out, key=lambda k: -k["ns"])
 
 
 # ---- bitcoin/message.go mirror --------------------------------------------

@@ -22,7 +22,7 @@ OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
 EXPORTS = (
     "mh_abi_version", "mh_device_count", "mh_search", "mh_search_multi", "mh_hash_batch",
     "mh_last_error", "mh_msg_encode", "mh_msg_decode", "mh_miner_handle",
-    "mh_profile_enable", "mh_profile_read", "mh_plan",
+    "mh_profile_enable", "mh_profile_read", "mh_profile_kernels", "mh_plan",
 )
 
 
@@ -30,6 +30,11 @@ class mh_piece(ctypes.Structure):
     _fields_ = [("first", ctypes.c_uint64), ("count", ctypes.c_uint64), ("kind", ctypes.c_int32),
                 ("digits", ctypes.c_int32), ("lo_digits", ctypes.c_int32), ("word", ctypes.c_int32),
                 ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32), ("nonce_ops", ctypes.c_uint32)]
+
+
+class mh_kernel_stat(ctypes.Structure):
+    _fields_ = [("word", ctypes.c_int32), ("mode", ctypes.c_int32), ("launches", ctypes.c_uint64),
+                ("nonces", ctypes.c_uint64), ("ns", ctypes.c_uint64), ("ops", ctypes.c_uint64)]
 
 
 class mh_message(ctypes.Structure):
@@ -61,6 +66,7 @@ def _load():
                                   ctypes.POINTER(sz)]
     L.mh_profile_enable.argtypes = [ctypes.c_int, ctypes.c_int]
     L.mh_profile_read.argtypes = [ctypes.c_int, u64p, ctypes.c_int]
+    L.mh_profile_kernels.argtypes = [ctypes.c_int, ctypes.POINTER(mh_kernel_stat), ctypes.c_int]
     L.mh_plan.argtypes = [u8p, sz, u64, u64, ctypes.POINTER(mh_piece), ctypes.c_int64]
     L.mh_plan.restype = ctypes.c_int64
     for name in EXPORTS:

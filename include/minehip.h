@@ -134,6 +134,17 @@ int mh_profile_enable(int dev, int on);
  * n = number of slots the caller provides (<= 8). */
 int mh_profile_read(int dev, uint64_t *out, int n);
 
+/* Per fast_search<J, MODE> variant counters since mh_profile_enable(dev, 1);
+ * the roofline's "dominant kernel" is the variant with the largest ns.  The
+ * kernel name in a rocprofv3 trace is `mh::fast_search<word, mode>`. */
+typedef struct mh_kernel_stat {
+    int32_t word, mode;
+    uint64_t launches, nonces, ns, ops;
+} mh_kernel_stat;
+
+/* Writes up to cap variants that ran; returns how many ran (or MH_E*). */
+int mh_profile_kernels(int dev, mh_kernel_stat *out, int cap);
+
 /* gfx950 VALU instructions of one full SHA-256 compression with no work
  * hoisted (64 rounds x 14 + 48 schedule words x 10). */
 #define MH_OPS_PER_BLOCK 1376u
