@@ -65,7 +65,7 @@ struct Timed {
 
 // per fast_search<J, MODE> variant: launches, nonces, ns, algorithmic instructions
 struct VarStat {
-    uint64_t launches = 0, nonces = 0, ns = 0, ops = 0;
+    uint64_t launches = 0, nonces = 0, ns = 0, ops = 0, slots = 0;
 };
 constexpr int kVariants = 48;  // J < 16, mode < 3
 
@@ -185,10 +185,12 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
             c->cnt[0] += 1;
             c->cnt[1] += p.count;
             c->cnt[3] += p.count * (uint64_t)p.ops;
+            c->cnt[6] += p.count * (uint64_t)p.slots;
             VarStat& v = c->var[p.J + 16 * p.mode];
             v.launches += 1;
             v.nonces += p.count;
             v.ops += p.count * (uint64_t)p.ops;
+            v.slots += p.count * (uint64_t)p.slots;
         } else {
             c->cnt[4] += p.count;
         }
@@ -373,9 +375,12 @@ int mh_profile_enable(int dev, int on) {
     rc = init_locked(c, dev);
     if (rc) return rc;
     MH_HIP(hipStreamSynchronize(c->stream));
-    c->used = 0;
-    memset(c->cnt, 0, sizeof c->cnt);
-    for (auto& v : c->var) v = VarStat();
+    rc = harvest_locked(c);  // timings of launches already recorded stay counted
+    if (rc) return rc;
+    if (on) {  // enabling starts a fresh count; disabling keeps the counts readable
+        memset(c->cnt, 0, sizeof c->cnt);
+        for (auto& v : c->var) v = VarStat();
+    }
     c->prof = on != 0;
     return MH_OK;
 }
@@ -419,6 +424,7 @@ int mh_profile_kernels(int dev, mh_kernel_stat* out, int cap) {
             out[n].nonces = v.nonces;
             out[n].ns = v.ns;
             out[n].ops = v.ops;
+            out[n].slots = v.slots;
         }
         ++n;
     }
@@ -451,6 +457,7 @@ int64_t mh_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, 
             q.mode = p.mode;
             q.blocks = p.blocks;
             q.nonce_ops = p.ops;
+            q.nonce_slots = p.slots;
         }
         ++k;
         return true;

@@ -110,39 +110,57 @@ void make_gen_args(const Prefix& pre, GenArgs* ga) {
     ga->t = pre.t;
 }
 
-uint32_t nonce_ops(int J, int mode) {
+NonceCost nonce_cost(int J, int mode) {
+    // Two counts of the same work:
+    //   ops   VALU instructions with gfx950's 3-input ops (v_alignbit, v_bitop3, v_add3);
+    //   slots issue slots of a SIMD-32 (2 cycles per wave64): full-rate ops
+    //         (v_bitop3, 2-input adds, shifts) take 1, v_alignbit takes 2, and a
+    //         sum costs one slot per addition (v_add3: 2 slots, 2 additions).
     // nonce-level words: those depending on word J (same rule as the kernel)
     uint64_t dep = 1ull << J;
     for (int t = 16; t < 64; ++t)
         if (((dep >> (t - 2)) | (dep >> (t - 7)) | (dep >> (t - 15)) | (dep >> (t - 16))) & 1ull) dep |= 1ull << t;
     auto is = [&](int t) { return (dep >> t) & 1ull; };
-    uint32_t ops = 0;
+    uint32_t ops = 0, slots = 0;
     for (int t = 16; t < 64; ++t) {
         if (!is(t)) continue;
-        // sigma: 2 alignbit + shift + xor3; the sum of n terms takes ceil((n-1)/2) add3
+        // sigma: 2 alignbit + shift + xor3 (4 ops, 6 slots); a sum of n terms:
+        // ceil((n-1)/2) add3 ops, n-1 slots
         const int s0 = (int)is(t - 15), s1 = (int)is(t - 2), a16 = (int)is(t - 16), a7 = (int)is(t - 7);
         const int hoisted = (s0 && s1 && a16 && a7) ? 0 : 1;  // group/run-level partial sum
         const int terms = s0 + s1 + a16 + a7 + hoisted;
         // sigma(W[J]) = sigma(wJ) ^ sigma(digit): one xor (the last digit never carries)
-        const uint32_t sig = (uint32_t)(s0 ? (t - 15 == J ? 1 : 4) : 0) + (uint32_t)(s1 ? (t - 2 == J ? 1 : 4) : 0);
-        ops += sig + (uint32_t)(terms - 1 + 1) / 2u;
+        const bool x0 = s0 && t - 15 == J, x1 = s1 && t - 2 == J;
+        ops += (uint32_t)((s0 ? (x0 ? 1 : 4) : 0) + (s1 ? (x1 ? 1 : 4) : 0)) + (uint32_t)terms / 2u;
+        slots += (uint32_t)((s0 ? (x0 ? 1 : 6) : 0) + (s1 ? (x1 ? 1 : 6) : 0)) + (uint32_t)(terms - 1);
     }
     // round J: T1 = hoisted + digit, e' and a' one add each
     ops += 3u;
-    // rounds J+1..63: 3+3 rotations, 2 xor3, Ch, Maj, 2 add3 for T1, e' add, a' add3 = 14;
-    // rounds J+1..J+3 read an invariant h and W, so h+K+W is hoisted (13)
-    for (int t = J + 1; t < 64; ++t) ops += (t <= J + 3 && !is(t)) ? 13u : 14u;
-    if (mode == kModeTwo) {
-        ops += 8u;                // feed-forward into block 1
-        ops += 64u * 14u - 1u;    // block 1 (its schedule is host-known); no e' in its last round
-    } else {
-        ops -= 1u;                // last round: e' is dead
+    slots += 3u;
+    // rounds J+1..63: 3+3 rotations, 2 xor3, Ch, Maj (16 slots) and the sums
+    //   T1 = h + S1 + Ch + K + W (4 additions; 3 when K+W is hoisted, 2 when h+K+W is),
+    //   e' = d + T1 (1), a' = T1 + S0 + Maj (2)
+    for (int t = J + 1; t < 64; ++t) {
+        const bool inv_w = !is(t), inv_h = inv_w && t <= J + 3;
+        ops += inv_h ? 13u : 14u;
+        slots += 16u + (inv_h ? 5u : inv_w ? 6u : 7u);
     }
-    // The last round's sum absorbs K[63] + st0, so H0 costs no extra add;
+    if (mode == kModeTwo) {
+        ops += 8u;                   // feed-forward into block 1
+        slots += 8u;
+        ops += 64u * 14u - 1u;       // block 1: schedule host-known, no e' in its last round;
+        slots += 64u * 22u - 1u;     // its last round also absorbs st0 (5 additions, 21 slots)
+    } else {
+        ops -= 1u;                   // last round: e' is dead, and K[63] + st0 rides in its sum
+        slots -= 1u;
+    }
     // H1 and the 64-bit compare run only on the rare new-best branch.
-    ops += 2u;                    // last digit into W[J], compare H0
-    return ops;
+    ops += 2u;                       // last digit into W[J], compare H0
+    slots += 2u;
+    return NonceCost{ops, slots};
 }
+
+uint32_t nonce_ops(int J, int mode) { return nonce_cost(J, mode).ops; }
 
 namespace {
 
@@ -270,7 +288,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             p.mode = mode;
             p.blocks = nb;
             p.fa = fa;
-            p.ops = nonce_ops(J, mode);
+            { const NonceCost nc = nonce_cost(J, mode); p.ops = nc.ops; p.slots = nc.slots; }
             p.fa.u_start = (uint64_t)u;
             p.fa.n_runs = (uint32_t)runs;
             p.ga = gbase;

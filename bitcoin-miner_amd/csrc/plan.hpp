@@ -40,7 +40,8 @@ struct Piece {
     int J;            // fast only
     int mode;         // fast only: FastMode
     int blocks;       // tail blocks of the final message
-    uint32_t ops;     // fast only: nonce_ops(J, mode)
+    uint32_t ops;     // fast only: nonce_cost(J, mode).ops
+    uint32_t slots;   // fast only: nonce_cost(J, mode).slots
     FastArgs fa;      // kind 0
     GenArgs ga;       // both (generic launch args; also used by hash_batch)
 };
@@ -64,6 +65,13 @@ void make_gen_args(const Prefix& pre, GenArgs* ga);
 // (14 per round, 4 per sigma, add3 sums); work shared by a group or a run is
 // amortised like the host midstate of SURVEY.md §8(d).  DESIGN.md §4.
 uint32_t nonce_ops(int J, int mode);
+
+// The same work in SIMD-32 issue slots (full-rate op 1, v_alignbit 2, one per
+// addition) -- the unit of the roofline peak, 128 lanes/clk/CU.
+struct NonceCost {
+    uint32_t ops, slots;
+};
+NonceCost nonce_cost(int J, int mode);
 
 int decimal_digits(uint64_t n);
 

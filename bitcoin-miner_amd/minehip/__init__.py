@@ -95,7 +95,7 @@ def profile_enable(dev=0, on=True):
 def profile_read(dev=0):
     out = (ctypes.c_uint64 * 8)()
     _check(lib.mh_profile_read(dev, out, 8))
-    keys = ("fast_launches", "fast_nonces", "fast_ns", "fast_ops", "generic_nonces", "generic_ns")
+    keys = ("fast_launches", "fast_nonces", "fast_ns", "fast_ops", "generic_nonces", "generic_ns", "fast_slots")
     return {k: int(out[i]) for i, k in enumerate(keys)}
 
 

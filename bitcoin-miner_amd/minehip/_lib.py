@@ -29,12 +29,14 @@ EXPORTS = (
 class mh_piece(ctypes.Structure):
     _fields_ = [("first", ctypes.c_uint64), ("count", ctypes.c_uint64), ("kind", ctypes.c_int32),
                 ("digits", ctypes.c_int32), ("lo_digits", ctypes.c_int32), ("word", ctypes.c_int32),
-                ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32), ("nonce_ops", ctypes.c_uint32)]
+                ("mode", ctypes.c_int32), ("blocks", ctypes.c_int32), ("nonce_ops", ctypes.c_uint32),
+                ("nonce_slots", ctypes.c_uint32)]
 
 
 class mh_kernel_stat(ctypes.Structure):
     _fields_ = [("word", ctypes.c_int32), ("mode", ctypes.c_int32), ("launches", ctypes.c_uint64),
-                ("nonces", ctypes.c_uint64), ("ns", ctypes.c_uint64), ("ops", ctypes.c_uint64)]
+                ("nonces", ctypes.c_uint64), ("ns", ctypes.c_uint64), ("ops", ctypes.c_uint64),
+                ("slots", ctypes.c_uint64)]
 
 
 class mh_message(ctypes.Structure):

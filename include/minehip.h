@@ -118,8 +118,8 @@ int mh_miner_handle(const int *devs, int ndev, const char *request, size_t len, 
 
 /* ---- measurement (no reference counterpart; used by bench.py) ---------- */
 
-/* Enable/disable HIP-event timing of every search-kernel launch on `dev`'s
- * stream, and reset the counters. */
+/* Enable (on != 0: counters reset) or disable (counters kept, readable) the
+ * HIP-event timing of every search-kernel launch on `dev`'s stream. */
 int mh_profile_enable(int dev, int on);
 
 /* Counters since the last mh_profile_enable(dev, 1):
@@ -131,6 +131,8 @@ int mh_profile_enable(int dev, int on);
  *          DESIGN.md §4); x64 lanes = int32 lane-ops
  *   out[4] nonces processed by the generic (edge) kernel
  *   out[5] generic kernel duration, nanoseconds
+ *   out[6] the same fast-kernel work in SIMD-32 issue slots: per piece,
+ *          nonces x mh_piece.nonce_slots (the roofline unit)
  * n = number of slots the caller provides (<= 8). */
 int mh_profile_read(int dev, uint64_t *out, int n);
 
@@ -139,7 +141,7 @@ int mh_profile_read(int dev, uint64_t *out, int n);
  * kernel name in a rocprofv3 trace is `mh::fast_search<word, mode>`. */
 typedef struct mh_kernel_stat {
     int32_t word, mode;
-    uint64_t launches, nonces, ns, ops;
+    uint64_t launches, nonces, ns, ops, slots;
 } mh_kernel_stat;
 
 /* Writes up to cap variants that ran; returns how many ran (or MH_E*). */
@@ -162,6 +164,7 @@ typedef struct mh_piece {
     int32_t mode;       /* fast: 0 one block, 1 prefix block per run, 2 two blocks per nonce */
     int32_t blocks;     /* tail blocks hashed per nonce in the final message */
     uint32_t nonce_ops; /* fast: algorithmic VALU instructions per nonce */
+    uint32_t nonce_slots; /* fast: the same work in SIMD-32 issue slots */
 } mh_piece;
 
 /* Plan the search of [lower, upper] for `msg`: writes the pieces in

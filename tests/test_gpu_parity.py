@@ -182,7 +182,8 @@ def test_profile_counters(gpu):
     assert p["fast_launches"] == len(fast) and p["fast_ns"] > 0
     assert p["fast_nonces"] + p["generic_nonces"] == 1 << 30
     assert p["fast_ops"] == sum(q["count"] * q["nonce_ops"] for q in fast)
-    ks = gpu.profile_kernels(0)
+    assert p["fast_slots"] == sum(q["count"] * q["nonce_slots"] for q in fast)
+    ks = gpu.profile_kernels(0)  # still readable after profile_enable(0, False)
     assert sum(k["launches"] for k in ks) == p["fast_launches"]
     assert sum(k["nonces"] for k in ks) == p["fast_nonces"]
     assert sum(k["ops"] for k in ks) == p["fast_ops"]
