@@ -13,10 +13,7 @@
 #include <string>
 
 #include "../../include/minehip.h"
-
-namespace mh {
-int set_error(int code, const char* what);
-}
+#include "msgcodec.hpp"
 
 namespace {
 
@@ -273,11 +270,9 @@ bool key_is(const std::string& k, const char* name) {  // Go: case-insensitive f
     return true;
 }
 
-struct Msg {
-    int64_t type = 0;
-    std::string data;
-    uint64_t lower = 0, upper = 0, hash = 0, nonce = 0;
-};
+}  // namespace
+
+namespace mh {
 
 bool decode(const char* js, size_t len, Msg* m) {
     Parser p{js, len};
@@ -344,6 +339,14 @@ std::string encode(int64_t type, const uint8_t* data, size_t dlen, uint64_t lowe
          ",\"Hash\":" + std::to_string(hash) + ",\"Nonce\":" + std::to_string(nonce) + "}";
     return o;
 }
+
+}  // namespace mh
+
+namespace {
+
+using mh::decode;
+using mh::encode;
+using mh::Msg;
 
 int copy_out(const std::string& s, char* out, size_t cap, size_t* out_len) {
     if (out_len) *out_len = s.size();

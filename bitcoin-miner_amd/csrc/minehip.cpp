@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -18,8 +20,10 @@
 #include <vector>
 
 #include "../../include/minehip.h"
+#include "../../include/minehip_server.h"
 #include "layout.hpp"
 #include "plan.hpp"
+#include "sched.hpp"
 
 namespace mh {
 hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
@@ -253,10 +257,6 @@ int check_common(const uint8_t* msg, size_t len) {
     return MH_OK;
 }
 
-inline bool lex_less(uint64_t ha, uint64_t na, uint64_t hb, uint64_t nb) {
-    return ha < hb || (ha == hb && na < nb);
-}
-
 }  // namespace
 
 extern "C" {
@@ -291,51 +291,83 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
         if (devs[i] < 0 || devs[i] >= n) return fail(n <= 0 ? MH_ENODEV : MH_EINVAL, "device index out of range");
     mh::Prefix pre;
     mh::absorb_prefix(msg, len, &pre);
-    const uint64_t span = upper - lower;  // count - 1
-    if (chunk == 0) {
-        // ~8 chunks per device for dynamic balance (buckets differ in cost),
-        // but >= 2^30 nonces (~33 ms) each so the per-chunk launch and sync
-        // overhead (~0.1 ms) stays under 1%
-        const uint64_t want = span / ((uint64_t)ndev * 8u) + 1u;
-        chunk = want < (1ull << 30) ? (1ull << 30) : want;
+    // One miner per listed device, fed by the server's scheduler (sched.hpp):
+    // chunks sized from each device's measured rate (~100 ms of work, >= 2^26
+    // nonces so the per-chunk launch + sync overhead of ~0.1 ms stays < 1%),
+    // capped at a fair share of what is left so the tail is spread over all
+    // devices.  A device that fails hands its chunk back to the others.
+    mh_sched_opts o;
+    mh_sched_default_opts(&o);
+    if (chunk) {
+        o.init_chunk = o.min_chunk = o.max_chunk = chunk;
+    } else {
+        o.min_chunk = 1ull << 26;
+        o.target_ns = 100000000ull;
     }
-    const uint64_t nchunks = span / chunk + 1u;  // chunk >= 1
-    std::atomic<uint64_t> next{0};
-    std::atomic<int> first_err{0};
-    std::vector<Partial> best((size_t)ndev, Partial{~0ull, ~0ull});
-    std::vector<std::string> errs((size_t)ndev);
+    mh::Scheduler sched(o);
+    for (int i = 0; i < ndev; ++i) sched.add_miner(i);
+    if (sched.submit(0, msg, len, lower, upper) < 0) return fail(MH_EINVAL, "internal: submit failed");
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;  // bumped on every completion or device loss
+    int alive = ndev, first_err = 0;
+    bool done = false;
+    mh_completion res{};
+    std::string err_msg;
+    auto now = []() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    };
     std::vector<std::thread> th;
     for (int i = 0; i < ndev; ++i) {
         th.emplace_back([&, i]() {
             for (;;) {
-                if (first_err.load() != 0) return;
-                const uint64_t k = next.fetch_add(1);
-                if (k >= nchunks) return;
-                const uint64_t a = lower + k * chunk;
-                const uint64_t b = (upper - a < chunk - 1u) ? upper : a + (chunk - 1u);
+                uint64_t seen;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (done) return;
+                    seen = gen;
+                }
+                mh_assignment a;
+                if (sched.next(i, now(), &a) != 1) {
+                    // nothing to hand out: wait for the job to finish, or for a
+                    // failed device's chunk to come back
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return done || gen != seen; });
+                    continue;
+                }
                 uint64_t h, nn;
-                const int r = search_impl(devs[i], pre, a, b, &h, &nn);
+                const int r = search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
                 if (r) {
-                    errs[(size_t)i] = g_err;
-                    int z = 0;
-                    first_err.compare_exchange_strong(z, r);
+                    const std::string e = g_err;
+                    sched.remove_miner(i);  // its chunk goes back to the job
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (!first_err) {
+                        first_err = r;
+                        err_msg = e;
+                    }
+                    if (--alive == 0) done = true;
+                    ++gen;
+                    cv.notify_all();
                     return;
                 }
-                if (lex_less(h, nn, best[(size_t)i].hash, best[(size_t)i].nonce)) best[(size_t)i] = Partial{h, nn};
+                mh_completion c;
+                const int q = sched.result(i, h, nn, now(), &c);
+                std::lock_guard<std::mutex> lk(mu);
+                if (q == 1) {
+                    res = c;
+                    done = true;
+                }
+                ++gen;
+                cv.notify_all();
             }
         });
     }
     for (auto& t : th) t.join();
-    if (first_err.load()) {
-        for (auto& e : errs)
-            if (!e.empty()) return fail(first_err.load(), e);
-        return fail(first_err.load(), "device worker failed");
-    }
-    Partial r = best[0];
-    for (int i = 1; i < ndev; ++i)
-        if (lex_less(best[(size_t)i].hash, best[(size_t)i].nonce, r.hash, r.nonce)) r = best[(size_t)i];
-    *out_hash = r.hash;
-    *out_nonce = r.nonce;
+    if (alive == 0) return fail(first_err ? first_err : MH_EHIP, err_msg.empty() ? "every device failed" : err_msg);
+    *out_hash = res.hash;
+    *out_nonce = res.nonce;
     return MH_OK;
 }
 

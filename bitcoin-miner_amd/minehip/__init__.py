@@ -181,3 +181,124 @@ def miner_handle(request_payload, devs=(0,)):
     buf = ctypes.create_string_buffer(256)
     _check(lib.mh_miner_handle(arr, len(devs), p, len(p), buf, 256, ctypes.byref(need)))
     return buf.raw[:need.value]
+
+
+# ---- bitcoin/server/server.go (stub :62) mirror: include/minehip_server.h ----
+from ._lib import mh_sched_opts, mh_assignment, mh_completion, mh_sched_stats  # noqa: E402
+
+
+def _opts(init_chunk=None, min_chunk=None, max_chunk=None, target_ns=None):
+    o = mh_sched_opts()
+    lib.mh_sched_default_opts(ctypes.byref(o))
+    for k, v in (("init_chunk", init_chunk), ("min_chunk", min_chunk), ("max_chunk", max_chunk),
+                 ("target_ns", target_ns)):
+        if v is not None:
+            setattr(o, k, v)
+    return o
+
+
+def _stats(fn, h):
+    st = mh_sched_stats()
+    _check(fn(h, ctypes.byref(st)))
+    return {f: int(getattr(st, f)) for f, _ in mh_sched_stats._fields_}
+
+
+def _chk_neg(rc):
+    if rc < 0:
+        _check(rc)
+    return rc
+
+
+class Scheduler:
+    """The server's chunk scheduler (mh_sched_*): jobs are client Requests,
+    chunks go to miners, Results merge by the lexicographic min.  Times are
+    caller-supplied nanoseconds."""
+
+    def __init__(self, **opts):
+        self._h = lib.mh_sched_create(ctypes.byref(_opts(**opts)))
+        if not self._h:
+            _check(MH_EINVAL)
+
+    def close(self):
+        if self._h:
+            lib.mh_sched_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def add_miner(self, miner):
+        _check(lib.mh_sched_add_miner(self._h, miner))
+
+    def remove_miner(self, miner):
+        _check(lib.mh_sched_remove_miner(self._h, miner))
+
+    def submit(self, client, msg, lower, upper):
+        m = _b(msg)
+        return _chk_neg(lib.mh_sched_submit(self._h, client, m, len(m), lower, upper))
+
+    def drop_client(self, client):
+        return _chk_neg(lib.mh_sched_drop_client(self._h, client))
+
+    def next(self, miner=-1, now=0):
+        """(miner, job, lower, upper) or None."""
+        a = mh_assignment()
+        if _chk_neg(lib.mh_sched_next(self._h, miner, now, ctypes.byref(a))) == 0:
+            return None
+        return a.miner, a.job, a.lower, a.upper
+
+    def job_msg(self, job):
+        n = ctypes.c_size_t()
+        buf = ctypes.create_string_buffer(MAX_MSG)
+        _check(lib.mh_sched_job_msg(self._h, job, buf, MAX_MSG, ctypes.byref(n)))
+        return buf.raw[:n.value]
+
+    def result(self, miner, hash_, nonce, now=0):
+        """(job, client, hash, nonce) when this Result finished its job, else None."""
+        c = mh_completion()
+        if _chk_neg(lib.mh_sched_result(self._h, miner, hash_, nonce, now, ctypes.byref(c))) == 0:
+            return None
+        return c.job, c.client, c.hash, c.nonce
+
+    def stats(self):
+        return _stats(lib.mh_sched_stats_read, self._h)
+
+
+MAX_MSG = 1 << 20  # MH_MAX_MSG_LEN
+
+
+class Server:
+    """The server's message loop (mh_server_*): feed it what lsp.Server.Read
+    returns, send what writes() yields with lsp.Server.Write."""
+
+    def __init__(self, **opts):
+        self._h = lib.mh_server_create(ctypes.byref(_opts(**opts)))
+        if not self._h:
+            _check(MH_EINVAL)
+        self._buf = ctypes.create_string_buffer(MAX_MSG + 256)
+
+    def close(self):
+        if self._h:
+            lib.mh_server_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def read(self, conn, payload, now=0):
+        p = _b(payload)
+        _check(lib.mh_server_read(self._h, conn, p, len(p), now))
+
+    def lost(self, conn, now=0):
+        _check(lib.mh_server_lost(self._h, conn, now))
+
+    def writes(self):
+        """Drain the queued writes: list of (conn, payload bytes)."""
+        out = []
+        conn = ctypes.c_int64()
+        n = ctypes.c_size_t()
+        while _chk_neg(lib.mh_server_pop_write(self._h, ctypes.byref(conn), self._buf, len(self._buf),
+                                               ctypes.byref(n))) == 1:
+            out.append((conn.value, self._buf.raw[:n.value]))
+        return out
+
+    def stats(self):
+        return _stats(lib.mh_server_stats, self._h)

@@ -1,4 +1,4 @@
-"""ctypes binding of libminehip.so (C-ABI: include/minehip.h).
+"""ctypes binding of libminehip.so (C-ABI: include/minehip.h, include/minehip_server.h).
 
 The library is built in-tree (``make`` at the repo root, or
 ``__graft_entry__.build()``) next to this file.  There is no fallback: if the
@@ -18,11 +18,17 @@ MH_ENODEV = -4
 MH_EHIP = -5
 OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
 
-#: every symbol include/minehip.h declares
+#: every symbol include/*.h declares
 EXPORTS = (
     "mh_abi_version", "mh_device_count", "mh_search", "mh_search_multi", "mh_hash_batch",
     "mh_last_error", "mh_msg_encode", "mh_msg_decode", "mh_miner_handle",
     "mh_profile_enable", "mh_profile_read", "mh_profile_kernels", "mh_plan",
+    # minehip_server.h
+    "mh_sched_default_opts", "mh_sched_create", "mh_sched_destroy", "mh_sched_add_miner",
+    "mh_sched_remove_miner", "mh_sched_submit", "mh_sched_drop_client", "mh_sched_next",
+    "mh_sched_job_msg", "mh_sched_result", "mh_sched_stats_read",
+    "mh_server_create", "mh_server_destroy", "mh_server_read", "mh_server_lost",
+    "mh_server_pop_write", "mh_server_stats",
 )
 
 
@@ -42,6 +48,27 @@ class mh_kernel_stat(ctypes.Structure):
 class mh_message(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int64), ("lower", ctypes.c_uint64), ("upper", ctypes.c_uint64),
                 ("hash", ctypes.c_uint64), ("nonce", ctypes.c_uint64), ("data_len", ctypes.c_size_t)]
+
+
+class mh_sched_opts(ctypes.Structure):
+    _fields_ = [("init_chunk", ctypes.c_uint64), ("min_chunk", ctypes.c_uint64),
+                ("max_chunk", ctypes.c_uint64), ("target_ns", ctypes.c_uint64)]
+
+
+class mh_assignment(ctypes.Structure):
+    _fields_ = [("miner", ctypes.c_int64), ("job", ctypes.c_int64), ("lower", ctypes.c_uint64),
+                ("upper", ctypes.c_uint64), ("msg_len", ctypes.c_size_t)]
+
+
+class mh_completion(ctypes.Structure):
+    _fields_ = [("job", ctypes.c_int64), ("client", ctypes.c_int64), ("hash", ctypes.c_uint64),
+                ("nonce", ctypes.c_uint64)]
+
+
+class mh_sched_stats(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in (
+        "miners", "idle_miners", "jobs", "chunks_assigned", "chunks_done", "chunks_requeued",
+        "nonces_done", "jobs_done", "jobs_cancelled")]
 
 
 def _load():
@@ -71,9 +98,30 @@ def _load():
     L.mh_profile_kernels.argtypes = [ctypes.c_int, ctypes.POINTER(mh_kernel_stat), ctypes.c_int]
     L.mh_plan.argtypes = [u8p, sz, u64, u64, ctypes.POINTER(mh_piece), ctypes.c_int64]
     L.mh_plan.restype = ctypes.c_int64
+    vp = ctypes.c_void_p
+    i64 = ctypes.c_int64
+    L.mh_sched_default_opts.argtypes = [ctypes.POINTER(mh_sched_opts)]
+    L.mh_sched_create.argtypes = [ctypes.POINTER(mh_sched_opts)]
+    L.mh_sched_destroy.argtypes = [vp]
+    L.mh_sched_add_miner.argtypes = [vp, i64]
+    L.mh_sched_remove_miner.argtypes = [vp, i64]
+    L.mh_sched_submit.argtypes = [vp, i64, u8p, sz, u64, u64]
+    L.mh_sched_drop_client.argtypes = [vp, i64]
+    L.mh_sched_next.argtypes = [vp, i64, u64, ctypes.POINTER(mh_assignment)]
+    L.mh_sched_job_msg.argtypes = [vp, i64, ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.mh_sched_result.argtypes = [vp, i64, u64, u64, u64, ctypes.POINTER(mh_completion)]
+    L.mh_sched_stats_read.argtypes = [vp, ctypes.POINTER(mh_sched_stats)]
+    L.mh_server_create.argtypes = [ctypes.POINTER(mh_sched_opts)]
+    L.mh_server_destroy.argtypes = [vp]
+    L.mh_server_read.argtypes = [vp, i64, ctypes.c_char_p, sz, u64]
+    L.mh_server_lost.argtypes = [vp, i64, u64]
+    L.mh_server_pop_write.argtypes = [vp, ctypes.POINTER(i64), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
+    L.mh_server_stats.argtypes = [vp, ctypes.POINTER(mh_sched_stats)]
+    restype = {"mh_plan": ctypes.c_int64, "mh_last_error": ctypes.c_char_p, "mh_sched_submit": i64,
+               "mh_sched_create": vp, "mh_server_create": vp, "mh_sched_default_opts": None,
+               "mh_sched_destroy": None, "mh_server_destroy": None}
     for name in EXPORTS:
-        if name not in ("mh_plan", "mh_last_error"):
-            getattr(L, name).restype = ctypes.c_int
+        getattr(L, name).restype = restype.get(name, ctypes.c_int)
     return L
 
 

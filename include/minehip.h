@@ -69,11 +69,15 @@ int mh_device_count(void);
 int mh_search(int dev, const uint8_t *msg, size_t len, uint64_t lower, uint64_t upper,
               uint64_t *out_hash, uint64_t *out_nonce);
 
-/* Same result, the range split into chunks handed out from a host work queue
- * to one host thread + HIP stream per listed device, merged on the host by the
- * same lexicographic min (associative, so bit-exact with mh_search).  No
- * device-to-device traffic: each device returns one 16-byte (hash, nonce).
- * chunk == 0 selects the default chunk size. */
+/* Same result, the range split into chunks by the server's scheduler
+ * (include/minehip_server.h) and handed to one host thread + HIP stream per
+ * listed device, merged on the host by the same lexicographic min
+ * (associative, so bit-exact with mh_search).  No device-to-device traffic:
+ * each chunk returns one 16-byte (hash, nonce).  chunk == 0: adaptive chunks
+ * (~100 ms of each device's measured rate, capped at a fair share of what is
+ * left); chunk > 0: fixed chunks of that many nonces.  A device that fails
+ * hands its chunk back to the others; the call fails only if every device
+ * fails (with the first failure's code). */
 int mh_search_multi(const int *devs, int ndev, const uint8_t *msg, size_t len, uint64_t lower,
                     uint64_t upper, uint64_t chunk, uint64_t *out_hash, uint64_t *out_nonce);
 

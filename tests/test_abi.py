@@ -16,7 +16,8 @@ U64 = (1 << 64) - 1
 
 
 def header_symbols():
-    src = open(os.path.join(ROOT, "include", "minehip.h")).read()
+    inc = os.path.join(ROOT, "include")
+    src = "".join(open(os.path.join(inc, f)).read() for f in sorted(os.listdir(inc)) if f.endswith(".h"))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(mh_[a-z_0-9]+)\s*\(", src)))
 

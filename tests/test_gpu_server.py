@@ -1,0 +1,68 @@
+"""GPU: the server loop (mh_server_*) driving GPU miners
+(mh_miner_handle: Request payload -> Result payload on the device), with a
+miner lost mid-job, against the oracle on small ranges and against a direct
+mh_search at BASELINE's 2^32 size (plus the re-hash property).  Bit-exact."""
+import json
+
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+U64 = (1 << 64) - 1
+
+
+def run_cluster(gpu, jobs, miners=(10, 11, 12), lose=None, **opts):
+    """Serve `jobs` [(client, msg, lo, hi)] with GPU miners; `lose` = a miner
+    that dies (without answering) after its first chunk.  Returns
+    {client: (hash, nonce)} and the server's stats."""
+    v = gpu.Server(**opts)
+    for m in miners:
+        v.read(m, gpu.marshal(gpu.NewJoin()))
+    for c, msg, lo, hi in jobs:
+        v.read(c, gpu.marshal(gpu.NewRequest(msg, lo, hi)))
+    results, t = {}, 0
+    pending = v.writes()
+    lost = False
+    while pending:
+        conn, payload = pending.pop(0)
+        t += 1
+        if conn in miners:
+            if conn == lose and not lost:
+                lost = True
+                v.lost(conn, now=t)           # dies holding this chunk
+            else:
+                v.read(conn, gpu.miner_handle(payload), now=t)
+        else:
+            m = json.loads(payload)
+            assert m["Type"] == 2
+            results[conn] = (m["Hash"], m["Nonce"])
+        pending += v.writes()
+    return results, v.stats()
+
+
+def test_server_small_ranges_vs_oracle(gpu):
+    jobs = [(1, b"cmu440", 0, 999_999), (2, b"x" * 60, 10 ** 9 - 5_000, 10 ** 9 + 300_000),
+            (3, b"a" * 100, U64 - 200_000, U64), (4, b"", 7, 7)]
+    res, st = run_cluster(gpu, jobs, lose=11, init_chunk=50_000, min_chunk=20_000, max_chunk=100_000)
+    for c, msg, lo, hi in jobs:
+        assert res[c] == oracle.search(msg, lo, hi, threads=8), c
+    assert st["chunks_requeued"] == 1 and st["jobs_done"] == 4 and st["jobs"] == 0
+
+
+def test_server_config2_size(gpu):
+    """BASELINE configs[1] range through the server, one miner lost."""
+    hi = (1 << 32) - 1
+    exp = gpu.search("cmu440", 0, hi)
+    res, st = run_cluster(gpu, [(1, "cmu440", 0, hi)], lose=12, init_chunk=1 << 28)
+    assert res[1] == exp
+    assert oracle.hash_("cmu440", exp[1]) == exp[0]
+    assert st["chunks_requeued"] == 1
+
+
+def test_search_multi_adaptive_and_fixed(gpu):
+    hi = (1 << 32) - 1
+    exp = gpu.search("cmu440", 0, hi)
+    assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0, 0, 0]) == exp       # adaptive chunks
+    assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0], chunk=(1 << 26) + 17) == exp

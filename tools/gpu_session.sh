@@ -32,6 +32,7 @@ for s in $STEPS; do
       make -C "$ROOT" -j16 all > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 1; }
       ;;
     tests)
+      make -C "$ROOT" -q all 2>/dev/null || echo "WARNING: build outputs older than sources" | tee -a "$OUT/session.log"
       timeout -k 10 900 python -m pytest "$ROOT/tests" -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/pytest_gpu.log"; fatal $rc
       ;;
@@ -88,6 +89,12 @@ for s in $STEPS; do
     latency)
       timeout -k 10 300 python "$ROOT/tools/latency.py" > "$OUT/latency.json" 2> "$OUT/latency.err"
       rc=$?; echo "latency rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/latency.json"; fatal $rc
+      ;;
+    cluster)
+      timeout -k 10 300 python "$ROOT/tools/cluster_bench.py" --bits 36 --miners 4 > "$OUT/cluster.json" 2> "$OUT/cluster.err"
+      rc=$?; echo "cluster rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/cluster.json"; fatal $rc
+      timeout -k 10 300 python "$ROOT/tools/cluster_bench.py" --bits 36 --miners 4 --lose > "$OUT/cluster_lose.json" 2> "$OUT/cluster_lose.err"
+      rc=$?; echo "cluster lose rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/cluster_lose.json"; fatal $rc
       ;;
     dist2)
       # 2 ranks on the box's one GPU over gloo: exercises bench.py's multi-process path
