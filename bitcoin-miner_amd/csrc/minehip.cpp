@@ -83,6 +83,7 @@ struct DevCtx {
     Partial* h_best = nullptr;  // pinned
     uint64_t* d_nonces = nullptr;
     uint64_t* d_hashes = nullptr;
+    uint32_t poff = 0;  // partials written since the last merge
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
@@ -153,8 +154,35 @@ int harvest_locked(DevCtx* c) {
     return MH_OK;
 }
 
-// Enqueue one piece (kernel + merge) on the context's stream.
+// Fold the pending partials into the running minimum.
+int flush_partials(DevCtx* c) {
+    if (c->poff) MH_HIP(mh::launch_merge(c->d_partials, c->poff, c->d_best, c->stream));
+    c->poff = 0;
+    return MH_OK;
+}
+
+// Enqueue one piece on the context's stream.  Its workgroups write their
+// partials after those of the previous pieces; one merge folds them all (or
+// earlier, when the buffer would overflow), instead of one merge per piece.
 int enqueue_piece(DevCtx* c, const mh::Piece& p) {
+    uint32_t blocks;
+    if (p.kind == 0) {
+        // host-side shape checks: the grid covers exactly n_runs lanes and the
+        // partials buffer holds one slot per block
+        if (p.fa.n_runs == 0 || p.fa.L < 1 || p.fa.L > 5 || p.fa.n_hi + p.fa.L > 20)
+            return fail(MH_EINVAL, "internal: bad fast piece");
+        blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
+    } else {
+        if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
+            return fail(MH_EINVAL, "internal: bad generic piece");
+        blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
+    }
+    if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINVAL, "internal: grid too large");
+    if (c->poff + blocks > mh::kMaxBlocksPerLaunch) {
+        const int rc = flush_partials(c);
+        if (rc) return rc;
+    }
+    Partial* out = c->d_partials + c->poff;
     Timed* tm = nullptr;
     if (c->prof) {
         if (c->used == kEventPairs) {
@@ -167,23 +195,12 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
         tm->var = p.J + 16 * p.mode;
         MH_HIP(hipEventRecord(tm->start, c->stream));
     }
-    uint32_t blocks;
-    if (p.kind == 0) {
-        // host-side shape checks: the grid covers exactly n_runs lanes and the
-        // partials buffer holds one slot per block
-        if (p.fa.n_runs == 0 || p.fa.L < 1 || p.fa.L > 5 || p.fa.n_hi + p.fa.L > 20)
-            return fail(MH_EINVAL, "internal: bad fast piece");
-        blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
-        if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINVAL, "internal: fast grid too large");
-        MH_HIP(mh::launch_fast(p.J, p.mode, p.fa, c->d_partials, blocks, c->stream));
-    } else {
-        if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
-            return fail(MH_EINVAL, "internal: bad generic piece");
-        blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
-        MH_HIP(mh::launch_generic_scan(p.ga, c->d_partials, blocks, c->stream));
-    }
+    if (p.kind == 0)
+        MH_HIP(mh::launch_fast(p.J, p.mode, p.fa, out, blocks, c->stream));
+    else
+        MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, c->stream));
     if (tm) MH_HIP(hipEventRecord(tm->stop, c->stream));
-    MH_HIP(mh::launch_merge(c->d_partials, blocks, c->d_best, c->stream));
+    c->poff += blocks;
     if (c->prof) {
         if (p.kind == 0) {
             c->cnt[0] += 1;
@@ -207,6 +224,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
 //   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 3)
 //   MINEHIP_MIN_LANES      lower L per bucket until it has this many runs (2^18)
 //   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^32)
+//   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -218,6 +236,7 @@ mh::PlanOpts plan_opts() {
         const unsigned long long v = strtoull(e, nullptr, 10);
         if (v >= 1) o.max_nonces_per_launch = v;
     }
+    if (const char* e = getenv("MINEHIP_GENERIC_BELOW")) o.generic_below = strtoull(e, nullptr, 10);
     return o;
 }
 
@@ -232,10 +251,12 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
     const mh::PlanOpts opt = plan_opts();
     int err = MH_OK;
+    c->poff = 0;
     mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
         err = enqueue_piece(c, p);
         return err == MH_OK;
     });
+    if (!err) err = flush_partials(c);
     if (err) {
         (void)hipStreamSynchronize(c->stream);
         return err;

@@ -225,21 +225,43 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
     const int d_lo = decimal_digits(lower), d_hi = decimal_digits(upper);
     const uint64_t max_gen = (uint64_t)kMaxBlocksPerLaunch * kBlockThreads;
 
-    auto emit_generic = [&](uint64_t a, uint64_t b, int d) -> bool {  // [a, b] inclusive, a <= b
+    // Generic pieces are coalesced across buckets (the generic kernel formats
+    // every nonce itself): small buckets and the ragged edges next to them go
+    // out as one launch instead of one launch + merge each.
+    bool have_gen = false;
+    uint64_t gen_a = 0, gen_b = 0;  // pending generic range, inclusive
+    auto flush_generic = [&]() -> bool {
+        if (!have_gen) return true;
+        have_gen = false;
+        Piece p;
+        memset(&p, 0, sizeof p);
+        p.first = gen_a;
+        p.count = gen_b - gen_a + 1u;
+        p.kind = 1;
+        p.digits = decimal_digits(gen_a);
+        p.blocks = ((pre.t + (uint32_t)decimal_digits(gen_b) + 9u) <= 64u) ? 1 : 2;
+        p.ga = gbase;
+        p.ga.first = gen_a;
+        p.ga.count = p.count;
+        return cb(p);
+    };
+    auto emit_generic = [&](uint64_t a, uint64_t b, int) -> bool {  // [a, b] inclusive, a <= b
         for (;;) {
-            const uint64_t left = b - a;  // count - 1
+            if (have_gen && gen_b - gen_a < max_gen - 1u && gen_b + 1u == a) {
+                const uint64_t room = max_gen - 1u - (gen_b - gen_a);  // nonces the pending piece can take
+                if (b - a < room) {
+                    gen_b = b;
+                    return true;
+                }
+                gen_b = a + (room - 1u);
+                a = gen_b + 1u;
+            }
+            if (!flush_generic()) return false;
+            const uint64_t left = b - a;
             const uint64_t cnt = (left >= max_gen - 1u) ? max_gen : left + 1u;
-            Piece p;
-            memset(&p, 0, sizeof p);
-            p.first = a;
-            p.count = cnt;
-            p.kind = 1;
-            p.digits = d;
-            p.blocks = ((pre.t + (uint32_t)d + 9u) <= 64u) ? 1 : 2;
-            p.ga = gbase;
-            p.ga.first = a;
-            p.ga.count = cnt;
-            if (!cb(p)) return false;
+            have_gen = true;
+            gen_a = a;
+            gen_b = a + (cnt - 1u);
             if (cnt - 1u == left) return true;
             a += cnt;
         }
@@ -257,7 +279,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         FastArgs fa;
         int J = 0, mode = 0, nb = 1;
         while (L >= 1 && !make_fast_args(pre, d, L, &J, &mode, &nb, &fa)) --L;
-        if (L < 1) {
+        if (L < 1 || B - A < opt.generic_below) {
             if (!emit_generic(A, B, d)) return;
             continue;
         }
@@ -271,6 +293,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const uint64_t fast_first = (uint64_t)(U0 * R);
         const unsigned __int128 fast_end = U1p * R;  // exclusive, may be 2^64
         if (A < fast_first && !emit_generic(A, fast_first - 1u, d)) return;
+        if (!flush_generic()) return;
         const uint64_t max_runs =
             std::max<uint64_t>(1u, std::min<uint64_t>((uint64_t)kMaxBlocksPerLaunch * kBlockThreads,
                                                       opt.max_nonces_per_launch / (uint64_t)R));
@@ -297,6 +320,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         }
         if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
     }
+    flush_generic();
 }
 
 }  // namespace mh

@@ -50,10 +50,13 @@ struct PlanOpts {
     int lower_digits = 3;                        // L upper bound (nonces per lane = 10^L)
     uint64_t min_lanes = 1u << 18;               // lower L until a bucket has this many runs
     uint64_t max_nonces_per_launch = 1ull << 32; // bounds one launch to ~0.1 s
+    uint64_t generic_below = 1u << 20;           // a bucket this small goes to the generic kernel whole
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb
-// returns false.  lower <= upper required.
+// returns false.  lower <= upper required.  A fast piece lies in one decimal
+// bucket; a generic piece may span several (contiguous small buckets and
+// edges are coalesced into one launch).
 void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
                  const std::function<bool(const Piece&)>& cb);
 

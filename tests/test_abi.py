@@ -77,9 +77,14 @@ def check_plan(msg, lo, hi):
         last = p["first"] + p["count"] - 1
         assert last <= hi
         d = p["digits"]
-        assert digits(p["first"]) == d and digits(last) == d, p  # one decimal bucket per piece
         t = plen % 64
-        assert p["blocks"] == (1 if t + d + 9 <= 64 else 2)
+        assert digits(p["first"]) == d, p
+        if p["kind"] == 1:  # generic: may span buckets (coalesced); blocks of its longest nonce
+            assert p["count"] <= 65536 * 256
+            assert p["blocks"] == (1 if t + digits(last) + 9 <= 64 else 2)
+        else:               # fast: one decimal bucket
+            assert digits(last) == d, p
+            assert p["blocks"] == (1 if t + d + 9 <= 64 else 2)
         if p["kind"] == 0:
             L = p["lo_digits"]
             R = 10 ** L
@@ -117,11 +122,22 @@ def test_plan_covers_exactly():
 def test_plan_uses_fast_kernel_for_bulk():
     pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
     fast = sum(p["count"] for p in pieces if p["kind"] == 0)
-    assert fast / 2 ** 32 > 0.9999
+    assert fast / 2 ** 32 > 0.999  # [0, 10^6) is one generic launch
     # long message, digits in the second tail block: per-run prefix block
     pieces = check_plan(b"x" * 60, 0, 2 ** 34 - 1)
     assert {p["mode"] for p in pieces if p["kind"] == 0} >= {1}
     assert sum(p["count"] for p in pieces if p["kind"] == 0) / 2 ** 34 > 0.9999
+
+
+def test_plan_coalesces_small_buckets():
+    # [0, 10^7): buckets d = 1..6 (10^6 nonces) in one generic launch, d = 7 fast
+    pieces = check_plan(b"cmu440", 0, 10 ** 7 - 1)
+    assert [(p["kind"], p["first"], p["count"]) for p in pieces] == [(1, 0, 10 ** 6), (0, 10 ** 6, 9 * 10 ** 6)]
+    # consecutive pieces never both generic (they would have been coalesced) unless one is full
+    for m in (b"", b"x" * 60, b"a" * 100):
+        ps = check_plan(m, 0, 2 ** 34 - 1)
+        for a, b in zip(ps, ps[1:]):
+            assert not (a["kind"] == 1 and b["kind"] == 1 and a["count"] < 65536 * 256)
 
 
 def test_plan_launch_cap():
@@ -189,8 +205,22 @@ KERNELS = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(13, 2), (
 
 
 def kernel_cases():
-    """One (msg, lo, hi) per instantiated fast kernel (word J, mode)."""
+    """One (msg, lo, hi) per instantiated fast kernel (word J, mode), planned
+    with MINEHIP_GENERIC_BELOW=0 (small buckets on the fast kernels)."""
     seen = {}
+    old = os.environ.get("MINEHIP_GENERIC_BELOW")
+    os.environ["MINEHIP_GENERIC_BELOW"] = "0"
+    try:
+        _kernel_cases(seen)
+    finally:
+        if old is None:
+            os.environ.pop("MINEHIP_GENERIC_BELOW")
+        else:
+            os.environ["MINEHIP_GENERIC_BELOW"] = old
+    return seen
+
+
+def _kernel_cases(seen):
     for L in range(0, 128):
         m = b"q" * L
         for d in range(2, 21):
@@ -199,7 +229,6 @@ def kernel_cases():
             for p in minehip.plan(m, lo, hi):
                 if p["kind"] == 0:
                     seen.setdefault((p["word"], p["mode"]), (m, lo, hi))
-    return seen
 
 
 def test_every_instantiated_kernel_is_reachable():

@@ -44,6 +44,13 @@ class env:
                 os.environ[k] = v
 
 
+def both_paths():
+    """Small ranges run once on the fast kernels (MINEHIP_GENERIC_BELOW=0) and
+    once as the default plan, which sends buckets < 2^20 nonces to the
+    generic kernel."""
+    return (env(MINEHIP_GENERIC_BELOW=0), env())
+
+
 def test_hash_batch_golden(gpu, golden_hash):
     by_msg = {}
     for m, n, h in golden_hash:
@@ -94,7 +101,10 @@ def test_every_tail_offset_and_bucket(gpu):
             c = 10 ** k
             lo = max(0, c - rng.randrange(1000, 9000))
             hi = min(U64, c + rng.randrange(3000, 14000))
-            assert gpu.search(m, lo, hi) == oracle.search(m, lo, hi, threads=8), (L, lo, hi)
+            exp = oracle.search(m, lo, hi, threads=8)
+            for e in both_paths():
+                with e:
+                    assert gpu.search(m, lo, hi) == exp, (L, lo, hi, e.kv)
 
 
 def test_every_kernel_instantiation(gpu):
@@ -108,22 +118,48 @@ def test_every_kernel_instantiation(gpu):
         hi = lo + 23_456
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 3):
-            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1):
+            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
                 assert gpu.search(m, lo, hi) == exp, (J, mode, len(m), Ld)
 
 
 def test_u64_edges(gpu):
     for m in (b"cmu440", b"", b"q" * 60, b"r" * 119):
-        assert gpu.search(m, U64, U64) == (oracle.hash_(m, U64), U64)
-        assert gpu.search(m, U64 - 30000, U64) == oracle.search(m, U64 - 30000, U64, threads=8)
-        assert gpu.search(m, 0, 0) == (oracle.hash_(m, 0), 0)
-        assert gpu.search(m, 0, 25000) == oracle.search(m, 0, 25000, threads=8)
+        top = oracle.search(m, U64 - 30000, U64, threads=8)
+        low = oracle.search(m, 0, 25000, threads=8)
+        for e in both_paths():
+            with e:
+                assert gpu.search(m, U64, U64) == (oracle.hash_(m, U64), U64)
+                assert gpu.search(m, U64 - 30000, U64) == top
+                assert gpu.search(m, 0, 0) == (oracle.hash_(m, 0), 0)
+                assert gpu.search(m, 0, 25000) == low
 
 
 def test_long_messages(gpu):
     for L in (191, 192, 300, 447, 600, 1000, 5000):
         m = bytes((i * 7 + 3) % 95 + 32 for i in range(L))
-        assert gpu.search(m, 999000, 1012000) == oracle.search(m, 999000, 1012000, threads=8), L
+        exp = oracle.search(m, 999000, 1012000, threads=8)
+        for e in both_paths():
+            with e:
+                assert gpu.search(m, 999000, 1012000) == exp, L
+
+
+def test_parity_fuzz_seed440(gpu):
+    """SURVEY §8(d) D2 parity fuzz: seed 440, message length 0..600, random
+    sub-ranges crossing 10^k and ranges ending at 2^64-1."""
+    rng = random.Random(440)
+    for i in range(60):
+        m = bytes(rng.randrange(0, 256) for _ in range(rng.randrange(0, 601)))
+        if i % 4 == 3:
+            hi = U64
+            lo = hi - rng.randrange(0, 40_000)
+        else:
+            c = 10 ** rng.randrange(1, 20)
+            lo = max(0, c - rng.randrange(0, 20_000))
+            hi = min(U64, c + rng.randrange(0, 20_000))
+        exp = oracle.search(m, lo, hi, threads=8)
+        for e in both_paths():
+            with e:
+                assert gpu.search(m, lo, hi) == exp, (len(m), lo, hi, e.kv)
 
 
 def test_plan_invariance_small(gpu):
@@ -132,8 +168,10 @@ def test_plan_invariance_small(gpu):
                       (b"a" * 100, 123, 345_678), (b"y" * 52, 10 ** 12 - 50_000, 10 ** 12 + 50_000)):
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 2, 3, 4, 5):
-            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000):
-                assert gpu.search(m, lo, hi) == exp, (m[:8], Ld)
+            for gb in (0, 1 << 20):
+                with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
+                         MINEHIP_GENERIC_BELOW=gb):
+                    assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb)
 
 
 @pytest.mark.parametrize("msg,bits", [(b"cmu440", 32), (b"a" * 100, 34), (b"x" * 60, 34)])
@@ -147,7 +185,7 @@ def test_full_size_properties(gpu, msg, bits):
     for _ in range(2):  # split-range associativity
         mid = rng.randrange(1, hi)
         assert lexmin(gpu.search(msg, 0, mid), gpu.search(msg, mid + 1, hi)) == r
-    with env(MINEHIP_LOWER_DIGITS=4, MINEHIP_MIN_LANES=1):
+    with env(MINEHIP_LOWER_DIGITS=4, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
         assert gpu.search(msg, 0, hi) == r
     with env(MINEHIP_LOWER_DIGITS=1, MINEHIP_LAUNCH_NONCES=1 << 28):
         assert gpu.search(msg, 0, hi) == r
