@@ -1,0 +1,41 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only).
+
+The planner, scheduler, server loop and Go-JSON codec of libminehip are
+compiled with g++ -fsanitize=address,undefined together with
+tests/host/fuzz_host.cpp, which drives them with randomized inputs (ranges up
+to 2^64-1, arbitrary bytes, random event orders) and checks their invariants.
+GPU sanitizers are not available on the MI355X pool; this covers the host side.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+CSRC = os.path.join(ROOT, "bitcoin-miner_amd", "csrc")
+SRCS = [os.path.join(CSRC, f) for f in ("plan.cpp", "sched.cpp", "server.cpp", "message.cpp")]
+DRIVER = os.path.join(ROOT, "tests", "host", "fuzz_host.cpp")
+
+
+@pytest.fixture(scope="module")
+def fuzz_bin(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    out = str(tmp_path_factory.mktemp("asan") / "fuzz_host")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", "-Wall", "-o", out, DRIVER] + SRCS
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return out
+
+
+@pytest.mark.parametrize("seed", [440, 1, 2])
+def test_host_fuzz_under_sanitizers(fuzz_bin, seed):
+    # verify_asan_link_order=0: the ASan runtime need not be the first DSO loaded
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([fuzz_bin, str(seed), "150"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "failures=0" in r.stdout
