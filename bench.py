@@ -238,7 +238,6 @@ def main():
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cfg["msg"], threads)
             cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, local))
-        from oracle import oracle
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -266,6 +265,9 @@ def main():
                 "unit": "T VALU lane issue-slots/s (int32)",
                 "frac": round(achieved / peak, 4) if peak else None,
                 "traffic": None,
+                "traffic_note": "PMC HBM bytes need their own rocprofv3 --pmc passes (tools/gpu_session.sh pmc, "
+                                "tools/pmc_summary.py): 678 KB per 100 ms d=10 launch in "
+                                "profiles/r01q_pmc_summary.json, ~0.1% of HBM bandwidth",
                 "kernel": dom["name"],
                 "launches": dom["launches"],
                 "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),
@@ -285,8 +287,10 @@ def main():
                                      "slots_per_nonce": round(prof["fast_slots"] / max(1, prof["fast_nonces"]), 1)},
             },
             "cpu_baseline": cpu,
+            # self-check on the product path: the winning nonce re-hashed by the
+            # generic kernel (mh_hash_batch), not the fast kernel that found it
             "result": {"hash": r[0], "nonce": r[1],
-                       "rehash_ok": oracle.hash_(msg, r[1]) == r[0]},
+                       "rehash_ok": minehip.Hash(msg, r[1], local) == r[0]},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
