@@ -340,6 +340,10 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
                    std::chrono::steady_clock::now().time_since_epoch())
             .count();
     };
+    // test hook: MINEHIP_TEST_FAIL_WORKER=i makes worker i's first search fail
+    // with MH_EHIP, to exercise the hand-back path on a one-GPU box
+    int fail_worker = -1;
+    if (const char* e = getenv("MINEHIP_TEST_FAIL_WORKER")) fail_worker = atoi(e);
     std::vector<std::thread> th;
     for (int i = 0; i < ndev; ++i) {
         th.emplace_back([&, i]() {
@@ -359,7 +363,8 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
                     continue;
                 }
                 uint64_t h, nn;
-                const int r = search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
+                const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (MINEHIP_TEST_FAIL_WORKER)")
+                                                 : search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
                 if (r) {
                     const std::string e = g_err;
                     sched.remove_miner(i);  // its chunk goes back to the job

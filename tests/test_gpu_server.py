@@ -66,3 +66,20 @@ def test_search_multi_adaptive_and_fixed(gpu):
     exp = gpu.search("cmu440", 0, hi)
     assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0, 0, 0]) == exp       # adaptive chunks
     assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0], chunk=(1 << 26) + 17) == exp
+
+
+def test_search_multi_device_failure_hand_back(gpu):
+    """A worker whose device fails hands its chunk back; the others finish
+    with the same answer.  If every worker fails, the call fails."""
+    import os
+    hi = (1 << 31) - 1
+    exp = gpu.search("cmu440", 0, hi)
+    os.environ["MINEHIP_TEST_FAIL_WORKER"] = "1"
+    try:
+        assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0, 0], chunk=1 << 27) == exp
+        os.environ["MINEHIP_TEST_FAIL_WORKER"] = "0"   # the only worker fails
+        with pytest.raises(gpu.MinehipError) as e:
+            gpu.search_multi("cmu440", 0, hi, devs=[0], chunk=1 << 27)
+        assert e.value.code == gpu.MH_EHIP and "injected" in str(e.value)
+    finally:
+        del os.environ["MINEHIP_TEST_FAIL_WORKER"]

@@ -64,6 +64,10 @@ for s in $STEPS; do
           -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc3.err")
       rc=$?; echo "pmc3 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       ;;
+    listpmc)
+      (cd /tmp && timeout -k 10 120 rocprofv3 -L > "$OUT/pmc_list.txt" 2>&1)
+      rc=$?; echo "listpmc rc=$rc" | tee -a "$OUT/session.log"; grep -c . "$OUT/pmc_list.txt"; fatal $rc
+      ;;
     valu)
       timeout -k 10 120 "$ROOT/build/valu_peak" > "$OUT/valu_peak.json" 2>&1
       rc=$?; echo "valu rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_peak.json"; fatal $rc
