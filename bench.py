@@ -18,9 +18,14 @@ region (mh_profile_*); `cpu_baseline` times the CPU port of the reference loop
 (oracle/) on a bounded sample, at N = 1 only.
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -141,6 +146,54 @@ def cpu_baseline(msg, threads):
     }
 
 
+def dominant_piece(msg, lo, hi, dom):
+    """The largest launch of the dominant fast_search<J, MODE> in this search's own plan."""
+    import minehip
+    ps = [p for p in minehip.plan(msg, lo, hi)
+          if p["kind"] == 0 and p["word"] == dom.get("word") and p["mode"] == dom.get("mode")]
+    return max(ps, key=lambda p: p["count"]) if ps else None
+
+
+def pmc_traffic(msg, piece, dev, timeout=90):
+    """HBM bytes of ONE launch of the dominant kernel, from rocprofv3 PMC counters:
+    two separate --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over
+    a child process (tools/pmc_launch.py) that searches exactly that launch's
+    nonces; bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB, the 2x being gfx950's
+    wide-read correction (MI355X_MICROARCH.md, HBM section).  Returns (bytes, note)."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    name = f"fast_search<{piece['word']}, {piece['mode']}>"
+    lo, hi = piece["first"], piece["first"] + piece["count"] - 1
+    vals = {}
+    work = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(work, counter)
+            cmd = [prof, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "pmc_launch.py"), msg, str(lo), str(hi), str(dev)]
+            try:
+                rc = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.PIPE).returncode
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {counter} timed out"
+            files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+            if rc != 0 or not files:
+                return None, f"rocprofv3 --pmc {counter} failed (rc {rc})"
+            per = {}
+            for r in csv.DictReader(open(files[0])):
+                if name in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                    per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+            if len(per) != 1:
+                return None, f"{len(per)} {name} dispatches in the --pmc {counter} pass, expected 1"
+            vals[counter] = next(iter(per.values()))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
+        f"FETCH_SIZE {vals['FETCH_SIZE']:.2f} KiB (x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.2f} KiB"
+
+
 def gpu_config1(search_dev):
     """BASELINE configs[0] on the GPU: wall ms of one [0, 9,999,999] search (median of 10)."""
     search_dev("cmu440", 0, 9_999_999)
@@ -161,6 +214,7 @@ def main():
     ap.add_argument("--msg", default=None, help="override the config's message")
     ap.add_argument("--bits", type=int, default=None, help="override log2 nonces per GPU (weak) / total (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes behind roofline.traffic")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="backend of the 16-byte merge and the timing max (nccl = RCCL on ROCm)")
     args = ap.parse_args()
@@ -232,6 +286,14 @@ def main():
     instr_achieved = dom["ops"] / (dom["ns"] * 1e-9) / 1e12 if dom["ns"] else 0.0
     all_achieved = prof["fast_slots"] / (prof["fast_ns"] * 1e-9) / 1e12 if prof["fast_ns"] else 0.0
 
+    traffic, traffic_note, alg_bytes = None, "not measured (N > 1 or --no-pmc)", None
+    piece = dominant_piece(msg, lo, hi, dom) if dom["name"] else None
+    if piece is not None:
+        runs = piece["count"] // 10 ** piece["lo_digits"]
+        alg_bytes = -(-runs // 256) * 16  # one 16-byte (hash, nonce) partial per 256-lane workgroup
+    if rank == 0 and world == 1 and not args.no_pmc and piece is not None:
+        traffic, traffic_note = pmc_traffic(cfg["msg"], piece, local)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -264,10 +326,10 @@ def main():
                 "peak": round(peak, 3),
                 "unit": "T VALU lane issue-slots/s (int32)",
                 "frac": round(achieved / peak, 4) if peak else None,
-                "traffic": None,
-                "traffic_note": "PMC HBM bytes need their own rocprofv3 --pmc passes (tools/gpu_session.sh pmc, "
-                                "tools/pmc_summary.py): 678 KB per 100 ms d=10 launch in "
-                                "profiles/r01q_pmc_summary.json, ~0.1% of HBM bandwidth",
+                "traffic": traffic,
+                "traffic_unit": "bytes per launch (HBM, PMC)",
+                "traffic_note": traffic_note,
+                "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel": dom["name"],
                 "launches": dom["launches"],
                 "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),

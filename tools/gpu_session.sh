@@ -46,22 +46,22 @@ for s in $STEPS; do
       ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+          -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
       ;;
     pmc)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
           -d "$OUT/pmc1" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc1.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc1.err")
       rc=$?; echo "pmc1 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace \
           -d "$OUT/pmc2" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc2.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc2.err")
       rc=$?; echo "pmc2 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
           -d "$OUT/pmc3" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> "$OUT/pmc3.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc3.err")
       rc=$?; echo "pmc3 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       ;;
     listpmc)
@@ -86,7 +86,7 @@ for s in $STEPS; do
       ;;
     benchcfg)
       for c in 3a 3b; do
-        timeout -k 10 600 python "$ROOT/bench.py" --config $c --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_cfg$c.json" 2> "$OUT/bench_cfg$c.err"
+        timeout -k 10 600 python "$ROOT/bench.py" --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-pmc > "$OUT/bench_cfg$c.json" 2> "$OUT/bench_cfg$c.err"
         rc=$?; echo "bench cfg $c rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_cfg$c.json"; fatal $rc
       done
       ;;
