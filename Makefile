@@ -10,10 +10,17 @@ SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSR
 HDRS    := $(CSRC)/layout.hpp $(CSRC)/plan.hpp $(CSRC)/sha256_gfx950.hpp $(CSRC)/msgcodec.hpp \
            $(CSRC)/sched.hpp include/minehip.h include/minehip_server.h
 
+LSPLIB  := $(PKG)/minehip/liblsp440.so
+APPS    := $(CSRC)/apps
 BIN     := $(PKG)/bin
-CLIS    := $(BIN)/minehip-search $(BIN)/minehip-miner
+CLIS    := $(BIN)/minehip-search $(BIN)/minehip-miner $(BIN)/minehip-server $(BIN)/minehip-client
+RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
-all: $(LIB) $(CLIS) oracle
+all: $(LIB) $(LSPLIB) $(CLIS) oracle
+
+# LSP endpoint (host only, wire compatible with the reference's Go lsp package)
+$(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
+	g++ -O2 -std=c++17 -Wall -Wextra -fPIC -shared -o $@ $(CSRC)/lsp/lsp.cpp -lpthread
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
@@ -21,10 +28,12 @@ $(LIB): $(SRCS) $(HDRS)
 # native C++ callers of the C-ABI (rpath: the library next to the package)
 $(BIN)/minehip-search: $(CSRC)/cli.cpp include/minehip.h $(LIB)
 	mkdir -p $(BIN)
-	g++ -O2 -std=c++17 -Wall -o $@ $(CSRC)/cli.cpp -L$(PKG)/minehip -lminehip -Wl,-rpath,'$$ORIGIN/../minehip'
+	g++ -O2 -std=c++17 -Wall -o $@ $(CSRC)/cli.cpp -L$(PKG)/minehip -lminehip $(RPATH)
 
-$(BIN)/minehip-miner: $(BIN)/minehip-search
-	ln -sf minehip-search $@
+# miner / server / client processes over LSP (bitcoin/{miner,server,client})
+$(BIN)/minehip-%: $(APPS)/%_main.cpp $(APPS)/common.hpp include/minehip.h include/minehip_server.h include/lsp440.h $(LIB) $(LSPLIB)
+	mkdir -p $(BIN)
+	g++ -O2 -std=c++17 -Wall -Wextra -o $@ $< -L$(PKG)/minehip -lminehip -llsp440 $(RPATH) -lpthread
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -35,7 +44,7 @@ asm: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
 clean:
-	rm -f $(LIB) $(CLIS)
+	rm -f $(LIB) $(LSPLIB) $(CLIS)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean

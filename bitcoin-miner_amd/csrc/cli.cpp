@@ -7,19 +7,12 @@
 //       (bitcoin/client/client.go:41-43), whose argument convention
 //       (client.go:12-19: <message> <maxNonce>) it follows minus the hostport.
 //
-//   minehip-miner
-//       the GPU miner's per-message step without the LSP transport: reads one
-//       JSON bitcoin.Message per line on stdin; for a Request
-//       (bitcoin/message.go:27-34) writes the Result JSON
-//       (message.go:38-44) on stdout; other lines are ignored, as a miner
-//       ignores non-Request messages.  The LSP wiring is the Go main in
-//       INTEGRATION.md.
+// The miner, server and client processes over LSP are apps/*_main.cpp.
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include <iostream>
 #include <string>
 #include <vector>
 
@@ -75,34 +68,8 @@ int run_search(int argc, char** argv) {
     return 0;
 }
 
-int run_miner() {
-    const std::vector<int> devs = all_devices();
-    if (devs.empty()) {
-        fprintf(stderr, "minehip: no HIP device\n");
-        return 1;
-    }
-    std::string line;
-    char out[256];
-    while (std::getline(std::cin, line)) {
-        size_t n = 0;
-        const int rc = mh_miner_handle(devs.data(), (int)devs.size(), line.data(), line.size(), out, sizeof out, &n);
-        if (rc == MH_EINVAL || rc == MH_ERANGE) continue;  // not a (valid) Request: ignored
-        if (rc != MH_OK) {
-            fprintf(stderr, "minehip: %s\n", mh_last_error());
-            return 1;
-        }
-        fwrite(out, 1, n, stdout);
-        fputc('\n', stdout);
-        fflush(stdout);
-    }
-    return 0;
-}
-
 }  // namespace
 
 int main(int argc, char** argv) {
-    const char* base = strrchr(argv[0], '/');
-    base = base ? base + 1 : argv[0];
-    if (strstr(base, "miner")) return run_miner();
     return run_search(argc, argv);
 }

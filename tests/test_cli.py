@@ -1,8 +1,10 @@
-"""Native C++ front ends of the C-ABI (bitcoin-miner_amd/csrc/cli.cpp).
+"""Native C++ front ends of the C-ABI (bitcoin-miner_amd/csrc/cli.cpp,
+csrc/apps/miner_main.cpp).
 
 minehip-search mirrors the reference client's arguments and output
-(bitcoin/client/client.go:12-19, :41-43); minehip-miner is the miner's
-Request -> Result step over JSON lines (bitcoin/message.go:27-44)."""
+(bitcoin/client/client.go:12-19, :41-43); `minehip-miner --stdio` is the
+miner's Request -> Result step over JSON lines (bitcoin/message.go:27-44).
+The processes over LSP are tested in test_e2e_cluster.py."""
 import os
 import subprocess
 
@@ -43,7 +45,7 @@ def test_miner_cli_json_lines(gpu):
         '{"Type":1,"Data":"cmu440","Lower":9,"Upper":3}',                        # Lower > Upper: ignored
         '{"Type":1,"Data":"","Lower":0,"Upper":0}',
     ]) + "\n"
-    r = run("minehip-miner", stdin=lines)
+    r = run("minehip-miner", "--stdio", stdin=lines)
     assert r.returncode == 0, r.stderr
     out = r.stdout.splitlines()
     assert out[0] == '{"Type":2,"Data":"","Lower":0,"Upper":0,"Hash":1228377698034,"Nonce":1067492}'

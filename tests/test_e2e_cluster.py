@@ -1,54 +1,77 @@
-"""End-to-end rehearsal of BASELINE configs[4] with tools/cluster.py: a server,
-miner processes and a client, with dropped-miner recovery.
+"""End-to-end BASELINE configs[4] layout over real LSP/UDP: the server, miner
+and client processes of the reference (bitcoin/server, bitcoin/miner,
+bitcoin/client), as separate OS processes
+on 127.0.0.1, with dropped-miner recovery.
 
-The pieces are separate OS processes exchanging Go-JSON bitcoin.Messages over a
-length-prefixed TCP framing on 127.0.0.1.  That framing stands in for the LSP
-transport, which is Go, unchanged, and not in this image.  The server is the
-library's mh_server loop.  One miner vanishes on receiving its first chunk;
-the client's printed Result must still equal a direct scan of the whole range.
+  server   bin/minehip-server <port>        libminehip's server loop over liblsp440
+  miners   bin/minehip-miner <hostport>     GPU (mh_miner_handle), or on CPU
+           tests/e2e_oracle_miner.py        the oracle over the same LSP
+  client   bin/minehip-client <hostport> <msg> <maxNonce>
 
-CPU: miners are tests/e2e_oracle_miner.py (the oracle, test infrastructure).
-GPU: miners are `tools/cluster.py miner` (mh_miner_handle on cuda:0)."""
+One miner disappears mid-job (it exits on its first Request, or is killed);
+the server learns of it through LSP's epoch timeout (Read -> (connID, err),
+the N3 fix) and hands its chunk to the others.  The client's printed Result
+must equal a direct scan of [0, maxNonce].  LSP_EPOCH_MILLIS shortens epochs
+so that loss is detected in ~0.5 s instead of EpochLimit x 2 s."""
 import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
-from conftest import ROOT
+from conftest import PKG, ROOT
 from oracle import oracle
 
 PY = sys.executable
-CLUSTER = os.path.join(ROOT, "tools", "cluster.py")
+BIN = os.path.join(PKG, "bin")
 ORACLE_MINER = os.path.join(ROOT, "tests", "e2e_oracle_miner.py")
+ENV = dict(os.environ, LSP_EPOCH_MILLIS="100", LSP_EPOCH_LIMIT="5")
 
 
-def free_port():
-    s = socket.socket()
+def free_udp_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
     s.close()
     return p
 
 
-def run_cluster(miners, msg, max_nonce, chunk, timeout):
-    """miners: list of (argv builder(hostport) -> argv).  Returns the client's
-    stdout and stderr; every process started here is killed afterwards."""
-    port = free_port()
+def run_cluster(miners, msg, max_nonce, chunk, timeout, kill_after=None, tmp=None):
+    """miners: argv builders (hostport -> argv).  kill_after = (index, seconds):
+    SIGKILL that miner that long after the client starts.  Returns the client's
+    stdout and the server's stderr.  Every process started here is killed by
+    PID afterwards."""
+    port = free_udp_port()
     hp = f"127.0.0.1:{port}"
+    env = dict(ENV, MINEHIP_CHUNK=str(chunk)) if chunk else ENV
+    err_path = os.path.join(tmp, "server.err")
     procs = []
     try:
-        srv = [PY, CLUSTER, "server", str(port)] + (["--chunk", str(chunk)] if chunk else [])
-        procs.append(subprocess.Popen(srv, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
-        for build in miners:
-            procs.append(subprocess.Popen(build(hp), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
-        cl = subprocess.run([PY, CLUSTER, "client", hp, msg, str(max_nonce)], capture_output=True, text=True,
-                            timeout=timeout)
-        return cl.stdout.strip(), cl.stderr
+        with open(err_path, "w") as serr:
+            srv = subprocess.Popen([os.path.join(BIN, "minehip-server"), str(port)], stdout=subprocess.PIPE,
+                                   stderr=serr, env=env, text=True)
+            procs.append(srv)
+            assert srv.stdout.readline().strip() == f"Server listening on port {port}"
+            miner_procs = []
+            for build in miners:
+                p = subprocess.Popen(build(hp), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
+                procs.append(p)
+                miner_procs.append(p)
+            time.sleep(0.5)  # let the miners join before the Request
+            cl = subprocess.Popen([os.path.join(BIN, "minehip-client"), hp, msg, str(max_nonce)],
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, text=True)
+            procs.append(cl)
+            if kill_after is not None:
+                time.sleep(kill_after[1])
+                miner_procs[kill_after[0]].kill()
+            out, _ = cl.communicate(timeout=timeout)
+        return out.strip(), open(err_path).read()
     finally:
         for p in procs:  # exactly the processes started here, by PID
-            p.kill()
+            if p.poll() is None:
+                p.kill()
             p.wait()
 
 
@@ -56,21 +79,59 @@ def oracle_miner(drop_after=0):
     return lambda hp: [PY, ORACLE_MINER, hp] + ([str(drop_after)] if drop_after else [])
 
 
-def gpu_miner(drop_after=0):
-    return lambda hp: [PY, CLUSTER, "miner", hp] + (["--drop-after", str(drop_after)] if drop_after else [])
+def gpu_miner():
+    return lambda hp: [os.path.join(BIN, "minehip-miner"), hp]
 
 
-def test_cluster_cpu_with_dropped_miner():
+def test_usage_lines():
+    r = subprocess.run([os.path.join(BIN, "minehip-client"), "x"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and r.stdout.startswith("Usage: ")
+    r = subprocess.run([os.path.join(BIN, "minehip-client"), "127.0.0.1:1", "m", "-3"], capture_output=True,
+                       text=True, timeout=30)
+    assert r.stdout == "-3 is not a number.\n"
+    r = subprocess.run([os.path.join(BIN, "minehip-server")], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and r.stdout.startswith("Usage: ")
+
+
+def test_client_without_server_fails_to_connect():
+    env = dict(ENV, LSP_EPOCH_MILLIS="50", LSP_EPOCH_LIMIT="2")
+    r = subprocess.run([os.path.join(BIN, "minehip-client"), f"127.0.0.1:{free_udp_port()}", "cmu440", "9"],
+                       capture_output=True, text=True, timeout=30, env=env)
+    assert r.stdout == "Failed to connect to server: can not establish connection\n"
+
+
+def test_client_sees_disconnected_when_server_dies(tmp_path):
+    port = free_udp_port()
+    srv = subprocess.Popen([os.path.join(BIN, "minehip-server"), str(port)], stdout=subprocess.PIPE,
+                           stderr=subprocess.DEVNULL, env=ENV, text=True)
+    try:
+        srv.stdout.readline()
+        cl = subprocess.Popen([os.path.join(BIN, "minehip-client"), f"127.0.0.1:{port}", "cmu440", "99"],
+                              stdout=subprocess.PIPE, text=True, env=ENV)
+        time.sleep(0.3)  # connected, Request sent; no miner, so no Result
+        srv.kill()
+        out, _ = cl.communicate(timeout=30)
+        assert out == "Disconnected\n"
+    finally:
+        if srv.poll() is None:
+            srv.kill()
+        srv.wait()
+
+
+def test_cluster_cpu_with_dropped_miner(tmp_path):
     out, err = run_cluster([oracle_miner(), oracle_miner(), oracle_miner(drop_after=1)],
-                           "cmu440", 1_999_999, chunk=100_000, timeout=240)
+                           "cmu440", 1_999_999, chunk=100_000, timeout=240, tmp=str(tmp_path))
     h, n = oracle.search("cmu440", 0, 1_999_999, threads=8)
     assert out == f"Result {h} {n}", err[-2000:]
+    assert "lost" in err  # the server saw the dropped miner through LSP
 
 
 @pytest.mark.gpu
-def test_cluster_gpu_with_dropped_miner(gpu):
-    max_nonce = (1 << 34) - 1
-    out, err = run_cluster([gpu_miner(), gpu_miner(), gpu_miner(drop_after=1)],
-                           "cmu440", max_nonce, chunk=1 << 30, timeout=600)
+def test_cluster_gpu_with_killed_miner(gpu, tmp_path):
+    # 3 GPU miner processes on the box's one GPU; one is SIGKILLed mid-job.
+    max_nonce = (1 << 36) - 1
+    out, err = run_cluster([gpu_miner(), gpu_miner(), gpu_miner()], "cmu440", max_nonce, chunk=1 << 31,
+                           timeout=600, kill_after=(2, 1.0), tmp=str(tmp_path))
     h, n = gpu.search("cmu440", 0, max_nonce)
     assert out == f"Result {h} {n}", err[-2000:]
+    assert "lost" in err and "requeued so far 0" not in err, err[-2000:]
