@@ -100,6 +100,12 @@ for s in $STEPS; do
       timeout -k 10 300 python "$ROOT/tools/cluster_bench.py" --bits 36 --miners 4 --lose > "$OUT/cluster_lose.json" 2> "$OUT/cluster_lose.err"
       rc=$?; echo "cluster lose rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/cluster_lose.json"; fatal $rc
       ;;
+    lspcluster)
+      timeout -k 10 300 python "$ROOT/tools/lsp_cluster_bench.py" --bits 38 --miners 1 > "$OUT/lsp_cluster.json" 2> "$OUT/lsp_cluster.err"
+      rc=$?; echo "lspcluster rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/lsp_cluster.json"; fatal $rc
+      timeout -k 10 300 python "$ROOT/tools/lsp_cluster_bench.py" --bits 38 --miners 2 --kill 2 > "$OUT/lsp_cluster_kill.json" 2> "$OUT/lsp_cluster_kill.err"
+      rc=$?; echo "lspcluster kill rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/lsp_cluster_kill.json"; fatal $rc
+      ;;
     dist2)
       # 2 ranks on the box's one GPU over gloo: exercises bench.py's multi-process path
       BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

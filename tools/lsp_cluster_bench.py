@@ -1,0 +1,87 @@
+"""Throughput of the whole process layout of BASELINE configs[4] over LSP/UDP
+on this box: bin/minehip-server, K bin/minehip-miner processes (GPU) and
+bin/minehip-client, against one direct mh_search of the same range.
+
+The client's wall time runs from its launch to its printed Result, so it
+includes LSP connect, the Request, every chunk's Request/Result round trip,
+JSON, scheduling and the final Result.  --kill SECONDS SIGKILLs one miner that
+long after the client starts (dropped-miner recovery: detected by LSP epoch
+timeout, LSP_EPOCH_MILLIS x LSP_EPOCH_LIMIT).
+
+    python tools/lsp_cluster_bench.py [--bits 38] [--miners 1] [--kill S]
+"""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
+BIN = os.path.join(ROOT, "bitcoin-miner_amd", "bin")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bits", type=int, default=38)
+    ap.add_argument("--miners", type=int, default=1)
+    ap.add_argument("--kill", type=float, default=None)
+    ap.add_argument("--msg", default="cmu440")
+    ap.add_argument("--epoch-ms", type=int, default=200)
+    a = ap.parse_args()
+    hi = (1 << a.bits) - 1
+
+    import minehip
+    minehip.search(a.msg, 0, 10 ** 6)
+    t0 = time.perf_counter()
+    direct = minehip.search(a.msg, 0, hi)
+    t_direct = time.perf_counter() - t0
+
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    hp = f"127.0.0.1:{port}"
+    env = dict(os.environ, LSP_EPOCH_MILLIS=str(a.epoch_ms), LSP_EPOCH_LIMIT="5")
+    procs = []
+    try:
+        srv = subprocess.Popen([os.path.join(BIN, "minehip-server"), str(port)], stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE, env=env, text=True)
+        procs.append(srv)
+        srv.stdout.readline()
+        miners = [subprocess.Popen([os.path.join(BIN, "minehip-miner"), hp], stdout=subprocess.DEVNULL,
+                                   stderr=subprocess.DEVNULL, env=env) for _ in range(a.miners)]
+        procs += miners
+        time.sleep(3.0)  # miners joined and their GPU contexts up
+        t0 = time.perf_counter()
+        cl = subprocess.Popen([os.path.join(BIN, "minehip-client"), hp, a.msg, str(hi)], stdout=subprocess.PIPE,
+                              env=env, text=True)
+        procs.append(cl)
+        if a.kill is not None:
+            time.sleep(a.kill)
+            miners[-1].kill()
+        out, _ = cl.communicate(timeout=3600)
+        t_lsp = time.perf_counter() - t0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    err = srv.stderr.read()
+    got = out.strip()
+    n = hi + 1
+    print(json.dumps({
+        "msg": a.msg, "nonces": n, "miners": a.miners, "killed_one_after_s": a.kill,
+        "epoch_ms": a.epoch_ms,
+        "direct": {"s": round(t_direct, 3), "ghs": round(n / t_direct / 1e9, 3), "result": list(direct)},
+        "lsp_cluster": {"s": round(t_lsp, 3), "ghs": round(n / t_lsp / 1e9, 3), "client_output": got},
+        "ratio": round(t_direct / t_lsp, 4),
+        "match": got == f"Result {direct[0]} {direct[1]}",
+        "server_log": err.strip().splitlines()[-3:],
+    }))
+
+
+if __name__ == "__main__":
+    main()
