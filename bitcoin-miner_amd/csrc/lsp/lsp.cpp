@@ -385,7 +385,10 @@ class Endpoint {
         if (timeout_ms < 0)
             cv_.wait(lk, ready);
         else
-            ok = cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready);
+            // system_clock: pthread_cond_timedwait, which ThreadSanitizer
+            // intercepts (GCC 11's TSan misses pthread_cond_clockwait, the
+            // steady-clock wait, and then reports false double locks)
+            ok = cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), ready);
         int rc;
         if (!events_.empty()) {
             Event& e = events_.front();

@@ -5,6 +5,10 @@ compiled with g++ -fsanitize=address,undefined together with
 tests/host/fuzz_host.cpp, which drives them with randomized inputs (ranges up
 to 2^64-1, arbitrary bytes, random event orders) and checks their invariants.
 GPU sanitizers are not available on the MI355X pool; this covers the host side.
+
+liblsp440 (bitcoin-miner_amd/csrc/lsp/lsp.cpp) is built with
+tests/host/fuzz_lsp.cpp twice: under address,undefined and under
+ThreadSanitizer (the reference's LSP tests are meant for `go test -race`).
 """
 import os
 import shutil
@@ -17,6 +21,8 @@ from conftest import ROOT
 CSRC = os.path.join(ROOT, "bitcoin-miner_amd", "csrc")
 SRCS = [os.path.join(CSRC, f) for f in ("plan.cpp", "sched.cpp", "server.cpp", "message.cpp")]
 DRIVER = os.path.join(ROOT, "tests", "host", "fuzz_host.cpp")
+LSP_SRC = os.path.join(CSRC, "lsp", "lsp.cpp")
+LSP_DRIVER = os.path.join(ROOT, "tests", "host", "fuzz_lsp.cpp")
 
 
 @pytest.fixture(scope="module")
@@ -39,3 +45,26 @@ def test_host_fuzz_under_sanitizers(fuzz_bin, seed):
     r = subprocess.run([fuzz_bin, str(seed), "150"], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "failures=0" in r.stdout
+
+
+@pytest.fixture(scope="module", params=["address,undefined", "thread"])
+def lsp_fuzz_bin(request, tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    san = request.param
+    out = str(tmp_path_factory.mktemp("lsp_" + san.split(",")[0]) / "fuzz_lsp")
+    extra = ["-fno-sanitize-recover=undefined"] if "undefined" in san else []
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}", *extra, "-Wall",
+           "-o", out, LSP_DRIVER, LSP_SRC, "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return out
+
+
+@pytest.mark.parametrize("seed", [440, 7])
+def test_lsp_under_sanitizers(lsp_fuzz_bin, seed):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1", TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([lsp_fuzz_bin, str(seed), "100"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "failures=0" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
