@@ -43,8 +43,18 @@ asm: $(SRCS) $(HDRS)
 	mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
+# VALU issue-rate microbenchmarks, run by tools/gpu_session.sh
+probes: build/valu_peak build/valu_ops build/valu_mix
+build/valu_mix: tools/gen_valu_mix.py
+	mkdir -p build
+	python3 tools/gen_valu_mix.py
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ tools/valu_mix.hip
+build/valu_%: tools/valu_%.hip
+	mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+
 clean:
 	rm -f $(LIB) $(LSPLIB) $(CLIS)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean probes
