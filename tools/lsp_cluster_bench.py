@@ -8,7 +8,12 @@ JSON, scheduling and the final Result.  --kill SECONDS SIGKILLs one miner that
 long after the client starts (dropped-miner recovery: detected by LSP epoch
 timeout, LSP_EPOCH_MILLIS x LSP_EPOCH_LIMIT).
 
-    python tools/lsp_cluster_bench.py [--bits 38] [--miners 1] [--kill S]
+    python tools/lsp_cluster_bench.py [--bits 38] [--miners 1] [--gpus G] [--kill S]
+
+--gpus G pins miner i to GPU i mod G (HIP_VISIBLE_DEVICES), one miner process per
+GPU as in configs[4]: on an 8-GPU node, `--bits 42 --miners 8 --gpus 8 --kill 5`
+is that config with a dropped miner.  --no-direct skips the direct-search
+reference timing (which uses one GPU only).
 """
 import argparse
 import json
@@ -30,14 +35,18 @@ def main():
     ap.add_argument("--kill", type=float, default=None)
     ap.add_argument("--msg", default="cmu440")
     ap.add_argument("--epoch-ms", type=int, default=200)
+    ap.add_argument("--gpus", type=int, default=0, help="pin miner i to GPU i mod GPUS (0: no pinning)")
+    ap.add_argument("--no-direct", action="store_true")
     a = ap.parse_args()
     hi = (1 << a.bits) - 1
 
-    import minehip
-    minehip.search(a.msg, 0, 10 ** 6)
-    t0 = time.perf_counter()
-    direct = minehip.search(a.msg, 0, hi)
-    t_direct = time.perf_counter() - t0
+    direct, t_direct = None, None
+    if not a.no_direct:
+        import minehip
+        minehip.search(a.msg, 0, 10 ** 6)
+        t0 = time.perf_counter()
+        direct = minehip.search(a.msg, 0, hi)
+        t_direct = time.perf_counter() - t0
 
     s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
     s.bind(("127.0.0.1", 0))
@@ -51,8 +60,11 @@ def main():
                                stderr=subprocess.PIPE, env=env, text=True)
         procs.append(srv)
         srv.stdout.readline()
-        miners = [subprocess.Popen([os.path.join(BIN, "minehip-miner"), hp], stdout=subprocess.DEVNULL,
-                                   stderr=subprocess.DEVNULL, env=env) for _ in range(a.miners)]
+        miners = []
+        for i in range(a.miners):
+            menv = dict(env, HIP_VISIBLE_DEVICES=str(i % a.gpus)) if a.gpus else env
+            miners.append(subprocess.Popen([os.path.join(BIN, "minehip-miner"), hp], stdout=subprocess.DEVNULL,
+                                           stderr=subprocess.DEVNULL, env=menv))
         procs += miners
         time.sleep(3.0)  # miners joined and their GPU contexts up
         t0 = time.perf_counter()
@@ -73,12 +85,13 @@ def main():
     got = out.strip()
     n = hi + 1
     print(json.dumps({
-        "msg": a.msg, "nonces": n, "miners": a.miners, "killed_one_after_s": a.kill,
+        "msg": a.msg, "nonces": n, "miners": a.miners, "gpus": a.gpus or None, "killed_one_after_s": a.kill,
         "epoch_ms": a.epoch_ms,
-        "direct": {"s": round(t_direct, 3), "ghs": round(n / t_direct / 1e9, 3), "result": list(direct)},
+        "direct": None if direct is None else {"s": round(t_direct, 3), "ghs": round(n / t_direct / 1e9, 3),
+                                               "result": list(direct)},
         "lsp_cluster": {"s": round(t_lsp, 3), "ghs": round(n / t_lsp / 1e9, 3), "client_output": got},
-        "ratio": round(t_direct / t_lsp, 4),
-        "match": got == f"Result {direct[0]} {direct[1]}",
+        "ratio": None if direct is None else round(t_direct / t_lsp, 4),
+        "match": None if direct is None else got == f"Result {direct[0]} {direct[1]}",
         "server_log": err.strip().splitlines()[-3:],
     }))
 
