@@ -68,3 +68,19 @@ def test_lsp_under_sanitizers(lsp_fuzz_bin, seed):
     r = subprocess.run([lsp_fuzz_bin, str(seed), "100"], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "failures=0" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
+
+
+def test_scheduler_under_thread_sanitizer(tmp_path):
+    """mh_sched_* from 6 miner threads + a submitter + churn (tests/host/tsan_sched.cpp)."""
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    out = str(tmp_path / "tsan_sched")
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-Wall", "-o", out,
+           os.path.join(ROOT, "tests", "host", "tsan_sched.cpp"), os.path.join(CSRC, "sched.cpp"), "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    for seed in (440, 7):
+        r = subprocess.run([out, str(seed)], capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+        assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+        assert "failures=0" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
