@@ -376,3 +376,54 @@ def test_client_close_waits_for_acks_under_loss():
     assert time.time() - t0 >= 0.2
     time.sleep(0.1)
     e.close()
+
+
+def test_server_slow_start():
+    # lsp3_test.go TestServerSlowStart: the client dials before the server is
+    # up; its Connect is resent every epoch until the server answers.
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()  # a free port, nobody listening yet
+    p = fast(limit=20, millis=50)
+    box = {}
+    t = threading.Thread(target=lambda: box.update(r=lsp.NewClient(f"127.0.0.1:{port}", p)))
+    t.start()
+    time.sleep(0.3)
+    srv, err = lsp.NewServer(port, p)
+    assert err is None
+    t.join(5)
+    cl, err = box["r"]
+    assert err is None and cl.ConnID() >= 1
+    assert cl.Write(b"late") is None
+    assert srv.Read(2000) == (cl.ConnID(), b"late", None)
+    cl.Close()
+    srv.Close()
+
+
+def test_every_client_ticks_independently():
+    # The reference server shares one time.Ticker among its per-client
+    # goroutines (lsp/server_impl.go:47,137), so each tick reaches one client
+    # and a loss stops it for all.  Here every connection is
+    # checked every epoch: two silent clients are both reported lost, and a
+    # third, live one is not.
+    p = fast(limit=3, millis=50)
+    srv, _ = lsp.NewServer(0, p)
+    a, _ = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    b, _ = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    live, _ = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    ids = {a.ConnID(), b.ConnID()}
+    a.Close()
+    b.Close()
+    lost = set()
+    t0 = time.time()
+    while len(lost) < 2 and time.time() - t0 < 3:
+        c, _, err = srv.Read(3000)
+        assert err is not None and err.code == lsp.LSP_ELOST
+        lost.add(c)
+    assert lost == ids
+    assert srv.Read(400)[2].code == lsp.LSP_ETIMEOUT  # the live client keeps heartbeating
+    assert live.Write(b"still here") is None
+    assert srv.Read(2000) == (live.ConnID(), b"still here", None)
+    live.Close()
+    srv.Close()
