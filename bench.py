@@ -109,6 +109,24 @@ def run_steps(search, lo, hi, steps, warmup, world, dist, torch, device, sync):
     return r, time.perf_counter() - t0
 
 
+def golden_expect(msg, lo, hi):
+    """The expected (hash, nonce) of [lo, hi] from the full-size fixtures
+    (tests/golden/fullsize_*.json, scanned with OpenSSL by gen_fullsize.py) when
+    [lo, hi] is a union of their chunks; None otherwise.  Data only: no oracle
+    code runs here."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "fullsize_*.json"))):
+        with open(path) as f:
+            d = json.load(f)
+        size = 1 << d["chunk_bits"]
+        if bytes.fromhex(d["msg_hex"]) != msg or lo < d["lo"] or hi > d["hi"]:
+            continue
+        if (lo - d["lo"]) % size or (hi + 1 - d["lo"]) % size:
+            continue
+        i, j = (lo - d["lo"]) // size, (hi + 1 - d["lo"]) // size
+        return min(tuple(c) for c in d["chunks"][i:j])
+    return None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -295,6 +313,10 @@ def main():
         traffic, traffic_note = pmc_traffic(cfg["msg"], piece, local)
 
     if rank == 0:
+        # the merged range of this run: every rank's shard
+        m_lo = min(rank_range(q, world, cfg["bits"], cfg["scaling"])[0] for q in range(world))
+        m_hi = max(rank_range(q, world, cfg["bits"], cfg["scaling"])[1] for q in range(world))
+        expect = golden_expect(msg, m_lo, m_hi)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
@@ -352,7 +374,10 @@ def main():
             # self-check on the product path: the winning nonce re-hashed by the
             # generic kernel (mh_hash_batch), not the fast kernel that found it
             "result": {"hash": r[0], "nonce": r[1],
-                       "rehash_ok": minehip.Hash(msg, r[1], local) == r[0]},
+                       "rehash_ok": minehip.Hash(msg, r[1], local) == r[0],
+                       "range": [m_lo, m_hi],
+                       # bit-exact against the full-size fixture when one covers the range
+                       "golden_ok": None if expect is None else tuple(r) == expect},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
