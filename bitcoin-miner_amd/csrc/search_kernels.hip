@@ -37,12 +37,44 @@ __device__ __forceinline__ bool lex_less(uint64_t ha, uint64_t na, uint64_t hb, 
     return ha < hb || (ha == hb && na < nb);
 }
 
+// One exchange step of the wave reduction: the partner's (hash, nonce),
+// fetched dword by dword by a DPP move (CTRL < 0x200) or a ds_swizzle
+// (CTRL >= 0x200: the swizzle offset - 0x200 is ADDED back below).
+template <int CTRL>
+__device__ __forceinline__ uint32_t xlane(uint32_t v) {
+    if constexpr (CTRL < 0x200)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+    else
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, CTRL - 0x200);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void wave_step(uint64_t& h, uint64_t& n) {
+    const uint64_t oh = ((uint64_t)xlane<CTRL>((uint32_t)(h >> 32)) << 32) | xlane<CTRL>((uint32_t)h);
+    const uint64_t on = ((uint64_t)xlane<CTRL>((uint32_t)(n >> 32)) << 32) | xlane<CTRL>((uint32_t)n);
+    if (lex_less(oh, on, h, n)) {
+        h = oh;
+        n = on;
+    }
+}
+
 // Workgroup lexicographic min; the result is valid in thread 0.
+// Wave level: DPP quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
+// row_mirror (each step joins two groups whose lanes already agree, so after
+// it every lane of the doubled group holds its min), then ds_swizzle xor 16
+// (bit mode, within 32 lanes), then lane 0 takes lane 32's value.  Then LDS
+// across the workgroup's waves.
 __device__ __forceinline__ void block_min(uint64_t& h, uint64_t& n) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t oh = __shfl_xor(h, off, 64);
-        const uint64_t on = __shfl_xor(n, off, 64);
+    wave_step<0xB1>(h, n);              // quad_perm [1,0,3,2]: lane ^ 1
+    wave_step<0x4E>(h, n);              // quad_perm [2,3,0,1]: lane ^ 2
+    wave_step<0x141>(h, n);             // row_half_mirror: quads of 8 lanes
+    wave_step<0x140>(h, n);             // row_mirror: halves of 16-lane rows
+    wave_step<0x200 + 0x401F>(h, n);    // ds_swizzle and 0x1F, xor 0x10: rows 0<->1, 2<->3
+    {
+        const uint64_t oh = ((uint64_t)__builtin_amdgcn_readlane((int)(h >> 32), 32) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, 32);
+        const uint64_t on = ((uint64_t)__builtin_amdgcn_readlane((int)(n >> 32), 32) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)n, 32);
         if (lex_less(oh, on, h, n)) {
             h = oh;
             n = on;
