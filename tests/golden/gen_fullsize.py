@@ -18,6 +18,10 @@ Configs (BASELINE.json configs):
          weak-scaling shards at N = 2/4/8 are [0, N*2^32-1], all covered.
   cfg3a  "a" * 100, [0, 2^34-1]: configs[2], host-midstate block.
   cfg3b  "x" * 60,  [0, 2^34-1]: configs[2], two tail blocks.
+  cfg4s  "cmu440", 2^24-nonce samples of configs[3]/[4] ([0, 2^40-1] and
+         [0, 2^42-1], digit buckets d = 11..13, too large to scan whole on a
+         CPU): 96 seeded random chunks, the chunks straddling 10^11 and
+         10^12, and the last chunks of [0, 2^40) and [0, 2^42).
 
 Run:  python tests/golden/gen_fullsize.py [cfg ...]   (~15 min on 8 cores)
 """
@@ -59,12 +63,43 @@ def hashlib_scan(msg, lo, hi):
     return best
 
 
+def sample_ranges():
+    import random
+    rng = random.Random(440)
+    size = 1 << CHUNK_BITS
+    los = {10 ** 11 - size // 2, 10 ** 12 - size // 2, (1 << 40) - size, (1 << 42) - size}
+    while len(los) < 100:
+        los.add(rng.randrange(1 << 35, (1 << 42) - size))
+    return [(lo, lo + size - 1) for lo in sorted(los)]
+
+
+def gen_samples(exe, threads, oracle):
+    msg = b"cmu440"
+    out = []
+    for lo, hi in sample_ranges():
+        r = subprocess.run([exe, msg.hex(), str(lo), str(hi), str(CHUNK_BITS - 3), str(threads)],
+                           check=True, capture_output=True, text=True)
+        out.append([lo, hi] + json.loads(r.stdout)["result"])
+    for lo, hi, h, n in (out[0], out[-1]):
+        assert oracle.search(msg, lo, hi, threads=threads) == (h, n)
+    path = os.path.join(HERE, "fullsize_cfg4s.json")
+    with open(path, "w") as f:
+        json.dump({"msg_hex": msg.hex(), "chunk_bits": CHUNK_BITS, "samples": out,
+                   "generator": "tests/golden/fullsize_scan.c (OpenSSL SHA-256), gen_fullsize.py",
+                   "cross_checked": "first and last sample vs oracle/sha256_oracle.c"}, f, separators=(",", ":"))
+        f.write("\n")
+    print(f"cfg4s: {len(out)} samples -> {path}", flush=True)
+
+
 def main(names):
     exe = build()
     threads = os.cpu_count() or 1
     sys.path.insert(0, ROOT)
     from oracle import oracle
     for name in names:
+        if name == "cfg4s":
+            gen_samples(exe, threads, oracle)
+            continue
         msg, lo, hi = CONFIGS[name]
         t = time.time()
         r = subprocess.run([exe, msg.hex(), str(lo), str(hi), str(CHUNK_BITS), str(threads)],
@@ -100,4 +135,4 @@ def main(names):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(CONFIGS))
+    main(sys.argv[1:] or list(CONFIGS) + ["cfg4s"])

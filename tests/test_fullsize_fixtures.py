@@ -39,3 +39,16 @@ def test_fixture_chunk_vs_oracle(name):
     i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000}[name]  # d = 10, 11, 11 chunks
     got = oracle.search(msg, i * size, (i + 1) * size - 1, threads=os.cpu_count() or 1)
     assert got == tuple(d["chunks"][i])
+
+
+def test_sample_fixture():
+    d = load_golden("fullsize_cfg4s.json")
+    assert bytes.fromhex(d["msg_hex"]) == b"cmu440" and len(d["samples"]) == 100
+    los = [s[0] for s in d["samples"]]
+    assert los == sorted(set(los))
+    for lo, hi, h, n in d["samples"]:
+        assert hi - lo + 1 == 1 << d["chunk_bits"] and lo <= n <= hi and hi < 1 << 42
+    for lo, hi, h, n in d["samples"][::33]:
+        assert oracle.hash_(b"cmu440", n) == h
+    lo, hi, h, n = d["samples"][50]
+    assert oracle.search(b"cmu440", lo, hi, threads=os.cpu_count() or 1) == (h, n)

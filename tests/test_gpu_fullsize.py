@@ -10,6 +10,7 @@ reproduce every one of them:
          d = 1..10) and the union of bench.py's weak-scaling shards at 8 GPUs
   cfg3a  "a" x 100 [0, 2^34-1]: configs[2], host-midstate block
   cfg3b  "x" x 60  [0, 2^34-1]: configs[2], two tail blocks
+  cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
 
 Reference semantics: bitcoin/hash.go:13-17 and the scan spec of SURVEY.md
 §8(a) A2 (reference stub bitcoin/miner/miner.go:33).
@@ -57,6 +58,14 @@ def test_config2_and_shards(gpu):
         exp = min(chunks[r * per:(r + 1) * per])
         assert gpu.search(msg, r << 32, ((r + 1) << 32) - 1) == exp, r
     assert gpu.search(msg, 0, (1 << 32) - 1) == min(chunks[:per])
+
+
+def test_config4_5_samples(gpu):
+    """configs[3]/[4] ranges ([0, 2^40-1], [0, 2^42-1]; d = 11..13): 100 OpenSSL-scanned 2^24 chunks."""
+    d = load_golden("fullsize_cfg4s.json")
+    msg = bytes.fromhex(d["msg_hex"])
+    bad = [(lo, hi) for lo, hi, h, n in d["samples"] if gpu.search(msg, lo, hi) != (h, n)]
+    assert not bad, bad[:3]
 
 
 def test_plan_knobs_full_size(gpu):
