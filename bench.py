@@ -172,12 +172,12 @@ def dominant_piece(msg, lo, hi, dom):
     return max(ps, key=lambda p: p["count"]) if ps else None
 
 
-def pmc_traffic(msg, piece, dev, timeout=90):
-    """HBM bytes of ONE launch of the dominant kernel, from rocprofv3 PMC counters:
-    two separate --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass) over
-    a child process (tools/pmc_launch.py) that searches exactly that launch's
-    nonces; bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB, the 2x being gfx950's
-    wide-read correction (MI355X_MICROARCH.md, HBM section).  Returns (bytes, note)."""
+def pmc_counters(msg, piece, dev, timeout=90):
+    """PMC counters of ONE launch of the dominant kernel: three separate rocprofv3
+    --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ_INSTS_VALU + GRBM_GUI_ACTIVE -- the
+    first two do not fit one pass) over a child process (tools/pmc_launch.py) that
+    searches exactly that launch's nonces.  Returns (values, error): values maps
+    each counter to its per-dispatch sum, plus "dur_ns" from the last pass."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"
@@ -187,29 +187,30 @@ def pmc_traffic(msg, piece, dev, timeout=90):
     work = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     try:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-            out = os.path.join(work, counter)
-            cmd = [prof, "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv", "--",
+        for counters in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]):
+            out = os.path.join(work, counters[0])
+            cmd = [prof, "--pmc", *counters, "-d", out, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.join(ROOT, "tools", "pmc_launch.py"), msg, str(lo), str(hi), str(dev)]
             try:
                 rc = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, stdout=subprocess.DEVNULL,
                                     stderr=subprocess.PIPE).returncode
             except subprocess.TimeoutExpired:
-                return None, f"rocprofv3 --pmc {counter} timed out"
+                return None, f"rocprofv3 --pmc {' '.join(counters)} timed out"
             files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
             if rc != 0 or not files:
-                return None, f"rocprofv3 --pmc {counter} failed (rc {rc})"
+                return None, f"rocprofv3 --pmc {' '.join(counters)} failed (rc {rc})"
             per = {}
             for r in csv.DictReader(open(files[0])):
-                if name in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                    per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                if name in r["Kernel_Name"] and r["Counter_Name"] in counters:
+                    d = per.setdefault(r["Dispatch_Id"], {})
+                    d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                    d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             if len(per) != 1:
-                return None, f"{len(per)} {name} dispatches in the --pmc {counter} pass, expected 1"
-            vals[counter] = next(iter(per.values()))
+                return None, f"{len(per)} {name} dispatches in the --pmc {' '.join(counters)} pass, expected 1"
+            vals.update(next(iter(per.values())))
     finally:
         shutil.rmtree(work, ignore_errors=True)
-    return int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), \
-        f"FETCH_SIZE {vals['FETCH_SIZE']:.2f} KiB (x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.2f} KiB"
+    return vals, None
 
 
 def gpu_config1(search_dev):
@@ -304,13 +305,29 @@ def main():
     instr_achieved = dom["ops"] / (dom["ns"] * 1e-9) / 1e12 if dom["ns"] else 0.0
     all_achieved = prof["fast_slots"] / (prof["fast_ns"] * 1e-9) / 1e12 if prof["fast_ns"] else 0.0
 
-    traffic, traffic_note, alg_bytes = None, "not measured (N > 1 or --no-pmc)", None
+    traffic, traffic_note, alg_bytes, pmc = None, "not measured (N > 1 or --no-pmc)", None, None
     piece = dominant_piece(msg, lo, hi, dom) if dom["name"] else None
     if piece is not None:
         runs = piece["count"] // 10 ** piece["lo_digits"]
         alg_bytes = -(-runs // 256) * 16  # one 16-byte (hash, nonce) partial per 256-lane workgroup
     if rank == 0 and world == 1 and not args.no_pmc and piece is not None:
-        traffic, traffic_note = pmc_traffic(cfg["msg"], piece, local)
+        vals, err = pmc_counters(cfg["msg"], piece, local)
+        if vals is None:
+            traffic_note = err
+        else:
+            # HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB, the 2x being gfx950's wide-read
+            # correction (MI355X_MICROARCH.md, HBM section)
+            traffic = int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024)
+            traffic_note = (f"FETCH_SIZE {vals['FETCH_SIZE']:.2f} KiB (x2 gfx950 correction), "
+                            f"WRITE_SIZE {vals['WRITE_SIZE']:.2f} KiB")
+            # clock the launch actually ran at: GRBM_GUI_ACTIVE is summed over the 8 XCDs
+            sclk = vals["GRBM_GUI_ACTIVE"] / 8 / vals["dur_ns"]
+            pmc = {"sclk_ghz": round(sclk, 3),
+                   "valu_instr_per_nonce": round(vals["SQ_INSTS_VALU"] * 64 / piece["count"], 1),
+                   "pmc_launch_ms": round(vals["dur_ns"] / 1e6, 3),
+                   "frac_at_sclk": round(achieved / (cus * SLOT_LANES_PER_CU_CLK * sclk * 1e9 / 1e12), 4),
+                   "note": "one launch of the dominant kernel under rocprofv3 --pmc SQ_INSTS_VALU "
+                           "GRBM_GUI_ACTIVE; frac_at_sclk = achieved / (CUs x 128 x sclk)"}
 
     if rank == 0:
         # the merged range of this run: every rank's shard
@@ -352,6 +369,7 @@ def main():
                 "traffic_unit": "bytes per launch (HBM, PMC)",
                 "traffic_note": traffic_note,
                 "algorithmic_bytes_per_launch": alg_bytes,
+                "pmc": pmc,
                 "kernel": dom["name"],
                 "launches": dom["launches"],
                 "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),
