@@ -11,7 +11,9 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "liboracle_sha256.so")
+_SO_OSSL = os.path.join(_HERE, "liboracle_openssl.so")
 _lib = None
+_lib_ossl = None
 
 
 def build():
@@ -77,4 +79,25 @@ def search(msg, lower, upper, threads=1):
         rc = lib().oracle_search_mt(m, len(m), lower, upper, threads, ctypes.byref(h), ctypes.byref(n))
     if rc != 0:
         raise ValueError("oracle_search: lower > upper")
+    return h.value, n.value
+
+
+def search_openssl(msg, lower, upper, threads=1):
+    """Optimised CPU scan (openssl_scan.c: midstate + OpenSSL SHA-256), same
+    answer as search(); bench.py's tuned CPU baseline."""
+    global _lib_ossl
+    if _lib_ossl is None:
+        if not os.path.exists(_SO_OSSL):
+            build()
+        L = ctypes.CDLL(_SO_OSSL)
+        u64 = ctypes.c_uint64
+        L.oracle_search_openssl.argtypes = [ctypes.c_char_p, ctypes.c_size_t, u64, u64, ctypes.c_int,
+                                            ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.oracle_search_openssl.restype = ctypes.c_int
+        _lib_ossl = L
+    m = _b(msg)
+    h = ctypes.c_uint64()
+    n = ctypes.c_uint64()
+    if _lib_ossl.oracle_search_openssl(m, len(m), lower, upper, threads, ctypes.byref(h), ctypes.byref(n)) != 0:
+        raise ValueError("oracle_search_openssl: lower > upper")
     return h.value, n.value

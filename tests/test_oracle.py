@@ -73,3 +73,15 @@ def test_scan_edges():
     hs = oracle.hash_batch("tie", np.arange(lo, hi + 1, dtype=np.uint64))
     k = int(np.argmin(hs))
     assert oracle.search("tie", lo, hi) == (int(hs[k]), lo + k)
+
+
+def test_openssl_scan_matches_restatement():
+    """oracle/openssl_scan.c (bench.py's tuned CPU baseline) answers like the restatement."""
+    U = (1 << 64) - 1
+    cases = [(b"cmu440", 0, 99_999), (b"cmu440", 9_990, 10_010), (b"", 0, 5_000), (b"x" * 60, 95_000, 105_000),
+             (b"a" * 100, 7, 7), (b"cmu440", U - 3_000, U), (bytes(range(256)), 10 ** 12 - 500, 10 ** 12 + 500)]
+    for msg, lo, hi in cases:
+        for threads in (1, 3):
+            assert oracle.search_openssl(msg, lo, hi, threads=threads) == oracle.search(msg, lo, hi), (msg[:8], lo, hi)
+    with pytest.raises(ValueError):
+        oracle.search_openssl(b"m", 5, 4)
