@@ -113,6 +113,13 @@ for s in $STEPS; do
           --dist-backend gloo > "$OUT/dist2.json" 2> "$OUT/dist2.err"
       rc=$?; echo "dist2 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist2.json"; fatal $rc
       ;;
+    dist8)
+      # 8 ranks on the box's one GPU over gloo: bench.py's N = 8 sharding and merge, golden-checked
+      BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+          --master-addr 127.0.0.1 --master-port 29534 "$ROOT/bench.py" --gpus 8 --steps 1 --warmup 1 \
+          --dist-backend gloo > "$OUT/dist8.json" 2> "$OUT/dist8.err"
+      rc=$?; echo "dist8 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8.json"; fatal $rc
+      ;;
     *) echo "unknown step $s";;
   esac
 done
