@@ -17,7 +17,7 @@
 namespace mh {
 
 constexpr int kBlockThreads = 256;         // 4 waves of 64 per workgroup
-constexpr uint32_t kMaxBlocksPerLaunch = 65536;
+constexpr uint32_t kMaxBlocksPerLaunch = 1u << 18;  // partials buffer slots; hard cap of one grid
 
 struct Partial {          // one (hash, nonce) candidate; ordered lexicographically
     uint64_t hash;

@@ -221,10 +221,11 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
 
 // Planner knobs, overridable for tests and tuning (the result never depends
 // on them -- tests/test_gpu_parity.py checks exactly that):
-//   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 3)
-//   MINEHIP_MIN_LANES      lower L per bucket until it has this many runs (2^18)
+//   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 2)
+//   MINEHIP_MIN_LANES      lower L per bucket until it has this many runs (2^23)
 //   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^32)
 //   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
+//   MINEHIP_MAX_BLOCKS     workgroups per launch (1..kMaxBlocksPerLaunch)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -237,6 +238,10 @@ mh::PlanOpts plan_opts() {
         if (v >= 1) o.max_nonces_per_launch = v;
     }
     if (const char* e = getenv("MINEHIP_GENERIC_BELOW")) o.generic_below = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("MINEHIP_MAX_BLOCKS")) {
+        const unsigned long long v = strtoull(e, nullptr, 10);
+        if (v >= 1 && v <= mh::kMaxBlocksPerLaunch) o.max_blocks = (uint32_t)v;
+    }
     return o;
 }
 

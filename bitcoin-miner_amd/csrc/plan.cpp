@@ -223,7 +223,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
     GenArgs gbase;
     make_gen_args(pre, &gbase);
     const int d_lo = decimal_digits(lower), d_hi = decimal_digits(upper);
-    const uint64_t max_gen = (uint64_t)kMaxBlocksPerLaunch * kBlockThreads;
+    const uint64_t max_gen = (uint64_t)std::min(opt.max_blocks, kMaxBlocksPerLaunch) * kBlockThreads;
 
     // Generic pieces are coalesced across buckets (the generic kernel formats
     // every nonce itself): small buckets and the ragged edges next to them go
@@ -273,8 +273,8 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         int L = std::min(opt.lower_digits, d - 1);
         L = std::min(L, 5);
         // A lane runs 10^L nonces serially: a bucket with few runs would leave
-        // most SIMDs idle and take one lane's latency, so shorten the runs
-        // until the bucket fills the GPU (min_lanes ~ 4 waves on every SIMD).
+        // most SIMDs idle and end in a long tail, so shorten the runs until
+        // the bucket has min_lanes of them (2^23: ~32 workgroups per CU).
         while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
         FastArgs fa;
         int J = 0, mode = 0, nb = 1;
@@ -295,7 +295,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         if (A < fast_first && !emit_generic(A, fast_first - 1u, d)) return;
         if (!flush_generic()) return;
         const uint64_t max_runs =
-            std::max<uint64_t>(1u, std::min<uint64_t>((uint64_t)kMaxBlocksPerLaunch * kBlockThreads,
+            std::max<uint64_t>(1u, std::min<uint64_t>(max_gen,
                                                       opt.max_nonces_per_launch / (uint64_t)R));
         for (unsigned __int128 u = U0; u < U1p;) {
             const unsigned __int128 left = U1p - u;

@@ -4,7 +4,7 @@
 // bitcoin/hash.go:13-17, scan spec SURVEY.md §8(a) A2 / stub
 // bitcoin/miner/miner.go:33).  Design: DESIGN.md §3.
 //
-//   fast_search<J, TWO>   one lane = one run of 10^L consecutive nonces that
+//   fast_search<J, MODE>  one lane = one run of 10^L consecutive nonces that
 //                         share their d-L higher digits; the L lower digits
 //                         are enumerated in wave-uniform loops (digit
 //                         arithmetic is SALU); only message word J (the last
@@ -15,7 +15,8 @@
 //                         buckets too small for runs).
 //   hash_batch            out[i] = Hash(msg, nonces[i]) (GPU bitcoin.Hash).
 //   merge_partials        folds per-workgroup (hash, nonce) candidates into
-//                         the search's running minimum (one workgroup).
+//                         the search's running minimum (one 1024-thread
+//                         workgroup).
 //
 // Every candidate comparison is the lexicographic (hash, nonce) order, which
 // equals the reference loop's strict-< first minimum.
@@ -38,8 +39,8 @@ __device__ __forceinline__ bool lex_less(uint64_t ha, uint64_t na, uint64_t hb, 
 }
 
 // One exchange step of the wave reduction: the partner's (hash, nonce),
-// fetched dword by dword by a DPP move (CTRL < 0x200) or a ds_swizzle
-// (CTRL >= 0x200: the swizzle offset - 0x200 is ADDED back below).
+// fetched dword by dword by a DPP move (CTRL < 0x200: CTRL is the dpp_ctrl)
+// or by a ds_swizzle (CTRL >= 0x200: the swizzle offset is CTRL - 0x200).
 template <int CTRL>
 __device__ __forceinline__ uint32_t xlane(uint32_t v) {
     if constexpr (CTRL < 0x200)
@@ -64,6 +65,7 @@ __device__ __forceinline__ void wave_step(uint64_t& h, uint64_t& n) {
 // it every lane of the doubled group holds its min), then ds_swizzle xor 16
 // (bit mode, within 32 lanes), then lane 0 takes lane 32's value.  Then LDS
 // across the workgroup's waves.
+template <int NT = kBlockThreads>
 __device__ __forceinline__ void block_min(uint64_t& h, uint64_t& n) {
     wave_step<0xB1>(h, n);              // quad_perm [1,0,3,2]: lane ^ 1
     wave_step<0x4E>(h, n);              // quad_perm [2,3,0,1]: lane ^ 2
@@ -80,7 +82,7 @@ __device__ __forceinline__ void block_min(uint64_t& h, uint64_t& n) {
             n = on;
         }
     }
-    __shared__ uint64_t sh[kBlockThreads / 64], sn[kBlockThreads / 64];
+    __shared__ uint64_t sh[NT / 64], sn[NT / 64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0) {
         sh[wv] = h;
@@ -89,7 +91,7 @@ __device__ __forceinline__ void block_min(uint64_t& h, uint64_t& n) {
     __syncthreads();
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int i = 1; i < kBlockThreads / 64; ++i)
+        for (int i = 1; i < NT / 64; ++i)
             if (lex_less(sh[i], sn[i], h, n)) {
                 h = sh[i];
                 n = sn[i];
@@ -443,18 +445,32 @@ __global__ __launch_bounds__(kBlockThreads) void hash_batch(const GenArgs a, con
     out[i] = ((uint64_t)h0 << 32) | h1;
 }
 
-__global__ __launch_bounds__(kBlockThreads) void merge_partials(const Partial* __restrict__ p, uint32_t n,
+// One workgroup of 1024 threads; each thread keeps 8 independent 16-byte
+// loads in flight, so folding a full 65,536-slot buffer (1 MiB) takes ~8
+// load round trips instead of 256 (the loop was latency-bound at 256 threads
+// and one load per iteration).
+constexpr int kMergeThreads = 1024;
+constexpr int kMergeUnroll = 8;
+
+__global__ __launch_bounds__(kMergeThreads) void merge_partials(const Partial* __restrict__ p, uint32_t n,
                                                                 Partial* __restrict__ best) {
     using namespace dev;
     uint64_t h = ~0ull, nn = ~0ull;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlockThreads) {
-        const Partial x = p[i];
-        if (lex_less(x.hash, x.nonce, h, nn)) {
-            h = x.hash;
-            nn = x.nonce;
+    for (uint32_t base = 0; base < n; base += kMergeThreads * kMergeUnroll) {
+        Partial x[kMergeUnroll];
+#pragma unroll
+        for (int u = 0; u < kMergeUnroll; ++u) {
+            const uint32_t i = base + (uint32_t)u * kMergeThreads + threadIdx.x;
+            x[u] = (i < n) ? p[i] : Partial{~0ull, ~0ull};
         }
+#pragma unroll
+        for (int u = 0; u < kMergeUnroll; ++u)
+            if (lex_less(x[u].hash, x[u].nonce, h, nn)) {
+                h = x[u].hash;
+                nn = x[u].nonce;
+            }
     }
-    block_min(h, nn);
+    block_min<kMergeThreads>(h, nn);
     if (threadIdx.x == 0) {
         const Partial b = *best;
         if (lex_less(h, nn, b.hash, b.nonce)) *best = Partial{h, nn};
@@ -519,7 +535,7 @@ hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_
 }
 
 hipError_t launch_merge(const Partial* partials, uint32_t n, Partial* best, hipStream_t s) {
-    hipLaunchKernelGGL(merge_partials, dim3(1), dim3(kBlockThreads), 0, s, partials, n, best);
+    hipLaunchKernelGGL(merge_partials, dim3(1), dim3(kMergeThreads), 0, s, partials, n, best);
     return hipGetLastError();
 }
 

@@ -80,7 +80,7 @@ def check_plan(msg, lo, hi):
         t = plen % 64
         assert digits(p["first"]) == d, p
         if p["kind"] == 1:  # generic: may span buckets (coalesced); blocks of its longest nonce
-            assert p["count"] <= 65536 * 256
+            assert p["count"] <= (1 << 17) * 256  # PlanOpts.max_blocks workgroups of 256
             assert p["blocks"] == (1 if t + digits(last) + 9 <= 64 else 2)
         else:               # fast: one decimal bucket
             assert digits(last) == d, p

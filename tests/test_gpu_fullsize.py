@@ -72,7 +72,7 @@ def test_plan_knobs_full_size(gpu):
     """The answer at 2^32 does not depend on the launch plan."""
     msg, _, _, bits, _, chunks = fixture("cfg2")
     exp = min(chunks[:(1 << 32) >> bits])
-    for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=2),
+    for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1 << 18),
                dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0)):
         with env(**kv):
             assert gpu.search(msg, 0, (1 << 32) - 1) == exp, kv
