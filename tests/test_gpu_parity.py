@@ -172,6 +172,10 @@ def test_plan_invariance_small(gpu):
                 with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
                          MINEHIP_GENERIC_BELOW=gb):
                     assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb)
+        # tiny grids: many launches per bucket and many partial-buffer flushes
+        for mb in (1, 3, 1000):
+            with env(MINEHIP_MAX_BLOCKS=mb, MINEHIP_MIN_LANES=1):
+                assert gpu.search(m, lo, hi) == exp, (m[:8], mb)
 
 
 @pytest.mark.parametrize("msg,bits", [(b"cmu440", 32), (b"a" * 100, 34), (b"x" * 60, 34)])
