@@ -1,8 +1,8 @@
-# Workgroups-per-launch A/B (MINEHIP_MAX_BLOCKS), kbench.py per line.
+# One vs two launch streams (MINEHIP_STREAMS): bench.py wall clock, interleaved runs.
 set -e
-mkdir -p gpurun_out/r01zo
-O=gpurun_out/r01zo/blocks.jsonl
-k() { timeout -k 10 200 python tools/kbench.py --rounds 4 "$@" --var b64k: --var b128k:MINEHIP_MAX_BLOCKS=131072 --var b256k:MINEHIP_MAX_BLOCKS=262144 >> $O; }
-k --msg cmu440 --lo 0 --count 4294967296
-k --msg cmu440 --lo 1000000000 --count 3294967296
-k --msg aaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaa --lo 0 --count 17179869184
+mkdir -p gpurun_out/r01zs
+for i in 1 2 3; do
+  for s in 1 2; do
+    MINEHIP_STREAMS=$s timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pmc > gpurun_out/r01zs/s${s}_$i.json
+  done
+done
