@@ -317,10 +317,32 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
         if (MH_R(t - 2)) v += ssig1(wr[t - 2]);
         if (MH_R(t)) wr[t] = v; else pr[t] = v;
     }
+    // K[t] + W[t] of the run-level words the per-nonce rounds read, made
+    // opaque so the register allocator keeps the sums instead of redoing the
+    // add on every nonce (it did, for t = 16..18, once the lane's best moved
+    // to SGPRs and freed VGPRs).
+    uint32_t kwr[64];
+#pragma unroll
+    for (int t = 16; t < 64; ++t)
+        if (MH_R(t) && t > J) {
+            kwr[t] = K[t] + wr[t];
+            asm volatile("" : "+v"(kwr[t]));
+        }
 
     const uint32_t lastpos = a.lo_pos + a.L - 1u;  // byte of the last digit, in word J
     const uint32_t sh_last = 24u - 8u * (lastpos & 3u);
-    uint32_t bh0 = 0xFFFFFFFFu, bh1 = 0xFFFFFFFFu, bq = 0u;
+    // The best (H0, H1, nonce) of the whole wave so far, wave-uniform (SGPRs).
+    // A lane is a candidate when its H0 <= the wave's best H0: the compare is
+    // already a lane mask, and the scan over its set bits is scalar work.
+    // Per wave, the candidate branch is taken ~ln(steps) times per run; per
+    // lane it was taken whenever any of 64 lanes improved its own minimum,
+    // ~64 + 64 ln(steps / 64) times, i.e. on ~93% of the steps of a 100-nonce
+    // run.  Invalid lanes (gid >= n_runs) never become candidates.
+    const uint64_t valid_mask = __builtin_amdgcn_ballot_w64(gid < a.n_runs);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t wave_u0 = a.u_start + (uint64_t)blockIdx.x * kBlockThreads + wave * 64u;
+    uint32_t wbh0 = 0xFFFFFFFFu, wbh1 = 0xFFFFFFFFu;
+    uint64_t wbn = ~0ull;
 
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
@@ -380,30 +402,40 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
             if constexpr (MODE != kModeTwo) {
 #pragma unroll
                 for (int t = J + 1; t < 63; ++t)
-                    round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
+                    round_kw(A, B, C, D, E, F, G, H,
+                             (t >= 16 && MH_R(t)) ? kwr[t] : K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
                 a63 = A;
                 h0 = last_round_h0(A, B, C, E, F, G, H,
                                    (K[63] + st[0]) + (MH_N(63) ? x[63] : (MH_G(63) ? wg[63] : wr[63])));
             } else {
 #pragma unroll
                 for (int t = J + 1; t < 64; ++t)
-                    round_kw(A, B, C, D, E, F, G, H, K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
+                    round_kw(A, B, C, D, E, F, G, H,
+                             (t >= 16 && MH_R(t)) ? kwr[t] : K[t] + (MH_N(t) ? x[t] : (MH_G(t) ? wg[t] : wr[t])));
                 const uint32_t s2[8] = {st[0] + A, st[1] + B, st[2] + C, st[3] + D,
                                         st[4] + E, st[5] + F, st[6] + G, st[7] + H};
                 sha256_block_kw_last(s2, a.kw1, h0, a63);  // block 1: padding + length only
                 a63 += s2[1] - st[1];                       // so that H1 = st[1] + a63 below
             }
-            // New best (rare after the first nonces): a real branch, not
-            // if-converted selects, so H1 and the 64-bit compare cost nothing
-            // on the common path.
-            if (__builtin_expect(h0 <= bh0, 0)) {
-                asm volatile("" ::);
+            // New wave best (rare): a uniform branch, so H1 and the
+            // lexicographic compare cost nothing on the common path.
+            const uint64_t cm = __builtin_amdgcn_ballot_w64(h0 <= wbh0) & valid_mask;
+            if (__builtin_expect(cm != 0ull, 0)) {
                 const uint32_t h1 = st[1] + a63;
-                if (h0 < bh0 || h1 < bh1) {
-                    bh0 = h0;
-                    bh1 = h1;
-                    bq = g * 10u + i;
-                }
+                const uint32_t q = g * 10u + i;
+                uint64_t m = cm;
+                do {
+                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1ull;
+                    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)h0, (int)l);
+                    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)h1, (int)l);
+                    const uint64_t cn = (wave_u0 + l) * a.pow10L + q;
+                    if (c0 < wbh0 || (c0 == wbh0 && (c1 < wbh1 || (c1 == wbh1 && cn < wbn)))) {
+                        wbh0 = c0;
+                        wbh1 = c1;
+                        wbn = cn;
+                    }
+                } while (m);
             }
         }
     }
@@ -411,12 +443,8 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 #undef MH_G
 #undef MH_R
 
-    uint64_t hash = ((uint64_t)bh0 << 32) | bh1;
-    uint64_t nonce = U * a.pow10L + bq;
-    if (gid >= a.n_runs) {
-        hash = ~0ull;
-        nonce = ~0ull;
-    }
+    uint64_t hash = ((uint64_t)wbh0 << 32) | wbh1;  // wave-uniform: the wave step of block_min
+    uint64_t nonce = wbn;                            // is a no-op, the LDS step joins the waves
     block_min(hash, nonce);
     if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
 }

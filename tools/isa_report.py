@@ -3,7 +3,7 @@
   make asm && python tools/isa_report.py build/search_kernels.s [filter]
 
 For every kernel: VGPRs/SGPRs/scratch from the metadata, and for the
-innermost loop (the per-nonce body of fast_search) the VALU instruction count,
+largest loop body (the per-nonce body of fast_search) the VALU instruction count,
 split into full-rate (1 issue slot) and half-rate (2 slots) instructions as
 measured by tools/valu_ops.hip on MI355X.
 """
@@ -45,7 +45,9 @@ def inner_loop(body):
     lines = body.split("\n")
     best = None
     for i, l in enumerate(lines):
-        if "Inner Loop Header" in l or ("Loop Header: Depth=1" in l and best is None):
+        # the per-nonce body is the loop block with the most VALU instructions (the
+        # innermost loop is the rare candidate scan of fast_search since r01zt)
+        if "Loop Header" in l:
             ins = []
             for j in range(i, len(lines)):
                 s = lines[j].strip()
