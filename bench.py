@@ -117,8 +117,15 @@ def golden_expect(msg, lo, hi):
     for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "fullsize_*.json"))):
         with open(path) as f:
             d = json.load(f)
+        if bytes.fromhex(d["msg_hex"]) != msg:
+            continue
+        for s_lo, s_hi, h, n in d.get("samples", []):  # sampled chunks (fullsize_cfg4s.json)
+            if (s_lo, s_hi) == (lo, hi):
+                return (h, n)
+        if "chunks" not in d:
+            continue
         size = 1 << d["chunk_bits"]
-        if bytes.fromhex(d["msg_hex"]) != msg or lo < d["lo"] or hi > d["hi"]:
+        if lo < d["lo"] or hi > d["hi"]:
             continue
         if (lo - d["lo"]) % size or (hi + 1 - d["lo"]) % size:
             continue

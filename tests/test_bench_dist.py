@@ -70,3 +70,19 @@ def test_rank_ranges_tile_the_space(world):
         assert rs[0][0] == 0 and all(rs[i][1] + 1 == rs[i + 1][0] for i in range(world - 1))
         total = (1 << bits) * (world if scaling == "weak" else 1)
         assert rs[-1][1] == total - 1
+
+
+def test_golden_expect_covers_every_bench_range():
+    """bench.py's result.golden_ok lookup: the merged range of configs[1] at N = 1, 2, 4, 8 and of
+    configs[2] at N = 1 come from the full-size fixtures; ranges no fixture covers give None
+    (configs[3]: 2^40), never an exception."""
+    for world in (1, 2, 4, 8):
+        lo = min(bench.rank_range(r, world, 32, "weak")[0] for r in range(world))
+        hi = max(bench.rank_range(r, world, 32, "weak")[1] for r in range(world))
+        assert bench.golden_expect(MSG, lo, hi) is not None, world
+    assert bench.golden_expect(MSG, 0, (1 << 32) - 1) == (3580905509, 4025695320)
+    for cfg in ("3a", "3b"):
+        c = bench.CONFIGS[cfg]
+        assert bench.golden_expect(c["msg"].encode(), 0, (1 << c["bits"]) - 1) is not None
+    assert bench.golden_expect(MSG, 0, (1 << 40) - 1) is None
+    assert bench.golden_expect(b"no fixture", 0, 99) is None
