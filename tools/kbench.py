@@ -11,7 +11,13 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
+# --pkg DIR: load the minehip package (and its libminehip.so) from DIR instead, e.g. an
+# experimental build (build/<variant>/minehip); must come first on the command line
+if len(sys.argv) > 2 and sys.argv[1] == "--pkg":
+    sys.path[:0] = [sys.argv[2]]
+    del sys.argv[1:3]
+else:
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
 import minehip  # noqa: E402
 
 
