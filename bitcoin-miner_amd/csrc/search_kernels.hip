@@ -216,7 +216,7 @@ constexpr IncSigma make_inc_sigma() {
         }
     return t;
 }
-__constant__ IncSigma kIncSigma = make_inc_sigma();
+static __constant__ IncSigma kIncSigma = make_inc_sigma();  // static: one copy per translation unit
 
 namespace dev {
 // Last round of a compression when only H0 = st0 + a64 is needed:
@@ -449,6 +449,7 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
     if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
 }
 
+#ifndef MH_PRE_TU  // the generic, batch and merge kernels live in the main translation unit
 __global__ __launch_bounds__(kBlockThreads) void generic_scan(const GenArgs a, Partial* __restrict__ partials) {
     using namespace dev;
     const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
@@ -505,6 +506,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_partials(const Partial* _
     }
 }
 
+#endif  // MH_PRE_TU
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -520,10 +523,25 @@ static hipError_t launch_fast_t(const FastArgs& a, Partial* partials, uint32_t b
     return hipGetLastError();
 }
 
-hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
 #define MH_CASE(j, m) \
     case j:           \
         return launch_fast_t<j, m>(a, partials, blocks, s);
+
+#ifdef MH_PRE_TU
+// Pre-mode instantiations (search_kernels_pre.hip): built with the default
+// AMDGPU scheduler, which orders their loop 0.35% faster than iterative-ilp
+// (the opposite of the One-mode kernels; profiles/r01zz7_sched.jsonl).
+hipError_t launch_fast_pre(int J, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
+    switch (J) {  // last digit at tail byte 64..82 (t <= 63, d <= 20): J <= 4
+        MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
+        MH_CASE(4, kModePre)
+        default: return hipErrorInvalidValue;
+    }
+}
+#else
+hipError_t launch_fast_pre(int J, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
+
+hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
     if (mode == kModeOne) {
         switch (J) {
             MH_CASE(0, kModeOne) MH_CASE(1, kModeOne) MH_CASE(2, kModeOne) MH_CASE(3, kModeOne)
@@ -533,20 +551,13 @@ hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, ui
             default: return hipErrorInvalidValue;
         }
     }
-    if (mode == kModePre) {  // last digit at tail byte 64..82 (t <= 63, d <= 20): J <= 4
-        switch (J) {
-            MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
-            MH_CASE(4, kModePre)
-            default: return hipErrorInvalidValue;
-        }
-    }
+    if (mode == kModePre) return launch_fast_pre(J, a, partials, blocks, s);
     if (mode == kModeTwo) {
         switch (J) {
             MH_CASE(13, kModeTwo) MH_CASE(14, kModeTwo) MH_CASE(15, kModeTwo)
             default: return hipErrorInvalidValue;
         }
     }
-#undef MH_CASE
     return hipErrorInvalidValue;
 }
 
@@ -566,5 +577,7 @@ hipError_t launch_merge(const Partial* partials, uint32_t n, Partial* best, hipS
     hipLaunchKernelGGL(merge_partials, dim3(1), dim3(kMergeThreads), 0, s, partials, n, best);
     return hipGetLastError();
 }
+#endif  // MH_PRE_TU
+#undef MH_CASE
 
 }  // namespace mh
