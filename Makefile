@@ -5,10 +5,6 @@ PKG     := bitcoin-miner_amd
 CSRC    := $(PKG)/csrc
 LIB     := $(PKG)/minehip/libminehip.so
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
-# AMDGPU machine scheduler for the kernels: "iterative-ilp" orders the per-nonce
-# loop of fast_search 1.6% faster than the default (same instructions, same
-# count; tools/kbench.py --pkg A/B, profiles/r01zz3_sched.jsonl)
-SCHEDFLAGS ?= -mllvm --amdgpu-sched-strategy=iterative-ilp
 SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSRC)/message.cpp \
            $(CSRC)/sched.cpp $(CSRC)/server.cpp
 HDRS    := $(CSRC)/layout.hpp $(CSRC)/plan.hpp $(CSRC)/sha256_gfx950.hpp $(CSRC)/msgcodec.hpp \
@@ -26,22 +22,8 @@ all: $(LIB) $(LSPLIB) $(CLIS) oracle
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
 	g++ -O2 -std=c++17 -Wall -Wextra -fPIC -shared -o $@ $(CSRC)/lsp/lsp.cpp -lpthread
 
-# the kernels: One/Two-mode fast_search, generic, batch and merge with SCHEDFLAGS;
-# the Pre-mode fast_search instantiations with the default scheduler (faster for them)
-OBJ     := build/obj
-KOBJS   := $(OBJ)/search_kernels.o $(OBJ)/search_kernels_pre.o
-HOSTSRC := $(filter-out $(CSRC)/search_kernels.hip,$(SRCS))
-
-$(OBJ)/search_kernels.o: $(CSRC)/search_kernels.hip $(HDRS)
-	mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) $(SCHEDFLAGS) -c -o $@ $<
-
-$(OBJ)/search_kernels_pre.o: $(CSRC)/search_kernels_pre.hip $(CSRC)/search_kernels.hip $(HDRS)
-	mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
-
-$(LIB): $(KOBJS) $(HOSTSRC) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(KOBJS) $(HOSTSRC)
+$(LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
 # native C++ callers of the C-ABI (rpath: the library next to the package)
 $(BIN)/minehip-search: $(CSRC)/cli.cpp include/minehip.h $(LIB)
@@ -59,8 +41,7 @@ oracle:
 # disassembly + register report of the kernels (for DESIGN.md / profiling)
 asm: $(SRCS) $(HDRS)
 	mkdir -p build
-	$(HIPCC) $(HIPFLAGS) $(SCHEDFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels_pre.s $(CSRC)/search_kernels_pre.hip
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
 # VALU issue-rate microbenchmarks, run by tools/gpu_session.sh
 probes: build/valu_peak build/valu_ops build/valu_mix

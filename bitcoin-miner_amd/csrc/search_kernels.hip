@@ -386,10 +386,10 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
             const uint32_t s0inc = kIncSigma.s0[sh_last >> 3][i], s1inc = kIncSigma.s1[sh_last >> 3][i];
             uint32_t x[64];
             x[J] = wJ + inc;
-            // schedule word t, computed right before the round that reads it: the
-            // iterative-ilp scheduler of the main translation unit ends with the same
-            // order either way, but the default scheduler of the Pre-mode one orders
-            // this source 1.5% faster (profiles/r01zz9_pre.jsonl)
+            // schedule word t, computed right before the round that reads it rather
+            // than all words first: the same instructions, but the AMDGPU scheduler
+            // then emits an order that issues 1.8% faster on configs[1] and 1.5% on
+            // the Pre-mode layouts (profiles/r01zz13_cur_vs_ildef.jsonl)
             auto sched = [&](int t) {
                 if (t < 16 || !MH_N(t)) return;
                 uint32_t v = pg[t];
@@ -457,7 +457,6 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
     if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
 }
 
-#ifndef MH_PRE_TU  // the generic, batch and merge kernels live in the main translation unit
 __global__ __launch_bounds__(kBlockThreads) void generic_scan(const GenArgs a, Partial* __restrict__ partials) {
     using namespace dev;
     const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
@@ -514,8 +513,6 @@ __global__ __launch_bounds__(kMergeThreads) void merge_partials(const Partial* _
     }
 }
 
-#endif  // MH_PRE_TU
-
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -535,20 +532,6 @@ static hipError_t launch_fast_t(const FastArgs& a, Partial* partials, uint32_t b
     case j:           \
         return launch_fast_t<j, m>(a, partials, blocks, s);
 
-#ifdef MH_PRE_TU
-// Pre-mode instantiations (search_kernels_pre.hip): built with the default
-// AMDGPU scheduler, which orders their loop 0.35% faster than iterative-ilp
-// (the opposite of the One-mode kernels; profiles/r01zz7_sched.jsonl).
-hipError_t launch_fast_pre(int J, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
-    switch (J) {  // last digit at tail byte 64..82 (t <= 63, d <= 20): J <= 4
-        MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
-        MH_CASE(4, kModePre)
-        default: return hipErrorInvalidValue;
-    }
-}
-#else
-hipError_t launch_fast_pre(int J, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
-
 hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
     if (mode == kModeOne) {
         switch (J) {
@@ -559,7 +542,13 @@ hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, ui
             default: return hipErrorInvalidValue;
         }
     }
-    if (mode == kModePre) return launch_fast_pre(J, a, partials, blocks, s);
+    if (mode == kModePre) {
+        switch (J) {  // last digit at tail byte 64..82 (t <= 63, d <= 20): J <= 4
+            MH_CASE(0, kModePre) MH_CASE(1, kModePre) MH_CASE(2, kModePre) MH_CASE(3, kModePre)
+            MH_CASE(4, kModePre)
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (mode == kModeTwo) {
         switch (J) {
             MH_CASE(13, kModeTwo) MH_CASE(14, kModeTwo) MH_CASE(15, kModeTwo)
@@ -585,7 +574,6 @@ hipError_t launch_merge(const Partial* partials, uint32_t n, Partial* best, hipS
     hipLaunchKernelGGL(merge_partials, dim3(1), dim3(kMergeThreads), 0, s, partials, n, best);
     return hipGetLastError();
 }
-#endif  // MH_PRE_TU
 #undef MH_CASE
 
 }  // namespace mh
