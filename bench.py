@@ -2,19 +2,41 @@
 """bench.py -- SHA-256 nonce-search throughput (BASELINE.json metric: GH/s at
 1/2/4/8 MI355X and % of the VALU integer roofline).
 
-One step = one search (the miner's scan over bitcoin.Hash, reference
-bitcoin/hash.go:13-17 + miner spec SURVEY.md §8(a) A2) of a 2^32-nonce shard of
-msg "cmu440" per GPU -- BASELINE.json configs[1] (single SHA block, nonces
-0..2^32-1 spanning every decimal-length bucket d = 1..10) at N = 1 -- followed by
-the 16-byte (hash, nonce) merge across ranks.  Weak scaling: rank r scans
-[r*2^32, (r+1)*2^32 - 1]; the only exchange is the 16-byte tuple per rank.
+A step is one search -- the miner's scan over bitcoin.Hash (reference
+bitcoin/hash.go:13-17; loop spec SURVEY.md §8(a) A2, stub bitcoin/miner/miner.go:33)
+-- of one batch of nonces, ending in the 16-byte (hash, nonce) host merge.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+Workloads (BASELINE.json configs; `--config` overrides the default):
+  N = 1  "2"  configs[1]: msg "cmu440", nonces [0, 2^32-1] every step (all
+              decimal buckets d = 1..10).  The metric's single-GPU line.
+  N > 1  "4"  configs[3]: msg "cmu440", nonces [0, 2^40-1] sharded over the N
+              GPUs with a host min-merge -- strong scaling.  The K timed steps
+              cover [0, 2^40-1] exactly once: step k scans the k-th of K equal
+              slices, split into N contiguous shards.  The merged result of the
+              timed region is configs[3]'s answer.
+  "3a"/"3b"   configs[2] (100 x 'a': host midstate; 60 x 'x': two tail blocks).
 
-Rank 0 prints ONE JSON line.  `roofline` comes from HIP events the library
-records around every fast-kernel launch on its own stream during the timed
-region (mh_profile_*); `cpu_baseline` times the CPU port of the reference loop
+How the N GPUs are driven (no RCCL, one 16-byte tuple per
+shard, merged on the host):
+  * launched (WORLD_SIZE > 1, e.g. `torch.distributed.run --nproc-per-node N
+    bench.py --gpus N`): one process per GPU -- the "one miner process per GPU"
+    layout of configs[4].  Rank r searches its shard on device LOCAL_RANK with
+    mh_search; the tuples, the barrier and the max-over-ranks time go over a
+    gloo (host) process group.  WORLD_SIZE must equal --gpus.
+  * self-contained (`python bench.py --gpus N`, no launcher): one process, one
+    host thread + HIP stream per device, mh_search_multi over devices 0..N-1
+    (the library's scheduler hands out chunks sized to each device's rate and
+    merges on the host).  Fewer than N visible devices is an error: exit 2, no
+    JSON line.  `--multi` forces this path at N = 1.
+
+Rank 0 prints ONE JSON line.  `roofline` is priced on SURVEY §8(d) D4's
+algorithmic basis (1,616 int32 VALU ops per SHA-256 compression x tail blocks
+per nonce) over the dominant kernel's HIP-event launch time, against the VALU
+peak 256 CU x 128 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: 4 SIMD-32 per CU);
+`roofline.slot_util` is the same kernel in the issue slots its compiled loop
+occupies.  At N = 1, rocprofv3 --pmc passes over one launch of
+each of the two largest kernels give HBM traffic and the SQ counters
+(`roofline.pmc`).  `cpu_baseline` times the CPU port of the reference loop
 (oracle/) on a bounded sample, at N = 1 only.
 """
 import argparse
@@ -35,15 +57,31 @@ for _p in (ROOT, os.path.join(ROOT, "bitcoin-miner_amd")):
 
 METRIC = "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of VALU int roofline"
 PEAK_SCLK_HZ = 2.4e9          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
-# VALU issue peak: 4 SIMD-32 per CU, a wave64 instruction every 2 cycles = 128
-# lane-slots/clk/CU (MI355X_MICROARCH.md, cdna_hip_programming.md §1).  Work is
-# counted in those slots: full-rate ops 1, half-rate v_alignbit/v_add3 2
-# (measured, tools/valu_ops.hip).
-SLOT_LANES_PER_CU_CLK = 128
-# Secondary view: instruction issue of a stream that mixes half-rate ops runs at
-# ~64 lanes/clk/CU whatever the mix (tools/gen_valu_mix.py).
-INSTR_LANES_PER_CU_CLK = 64
-OPS_PER_BLOCK = 1376          # gfx950 VALU instructions of one un-hoisted SHA-256 compression
+# VALU peak: 4 SIMD-32 per CU, a wave64 instruction every 2 cycles = 128
+# int32 lane-ops/clk/CU (MI355X_MICROARCH.md "Wave scheduling").
+LANES_PER_CU_CLK = 128
+# canonical gfx950 VALU ops of one SHA-256 compression.
+# Ops per hash = 1,616 x tail blocks; host-midstate blocks are excluded.
+SURVEY_OPS_PER_COMPRESSION = 1616
+OPS_PER_BLOCK = 1376          # this kernel's count for an un-hoisted compression (v_bitop3 xor3)
+
+# BASELINE.json configs as bench workloads.
+CONFIGS = {
+    "2": dict(msg="cmu440", bits=32, scaling="weak",
+              desc="BASELINE configs[1]: single SHA block, nonces [0, 2^32-1] per GPU per step "
+                   "(all buckets d=1..10 at N=1)"),
+    "3a": dict(msg="a" * 100, bits=34, scaling="weak",
+               desc="BASELINE configs[2]: 100-byte msg (host midstate block), 2^34 nonces per GPU per step"),
+    "3b": dict(msg="x" * 60, bits=34, scaling="weak",
+               desc="BASELINE configs[2]: 60-byte msg (two tail blocks), 2^34 nonces per GPU per step"),
+    "4": dict(msg="cmu440", bits=40, scaling="strong",
+              desc="BASELINE configs[3]: nonces [0, 2^40-1] sharded over the GPUs, host min-merge; "
+                   "the K timed steps are K equal slices covering the range once"),
+}
+
+
+def default_config(gpus):
+    return "2" if gpus == 1 else "4"
 
 
 def shard(rank, bits):
@@ -51,28 +89,35 @@ def shard(rank, bits):
     return lo, lo + (1 << bits) - 1
 
 
-# BASELINE.json configs as bench workloads.  "2" (configs[1]) is the default and
-# the one the metric is quoted on; the others are for DESIGN.md's tables.
-CONFIGS = {
-    "2": dict(msg="cmu440", bits=32, scaling="weak",
-              desc="BASELINE configs[1]: single SHA block, 2^32 nonces per GPU (all buckets d=1..10 at N=1)"),
-    "3a": dict(msg="a" * 100, bits=34, scaling="weak",
-               desc="BASELINE configs[2]: 100-byte msg (host midstate block), 2^34 nonces per GPU"),
-    "3b": dict(msg="x" * 60, bits=34, scaling="weak",
-               desc="BASELINE configs[2]: 60-byte msg (two tail blocks), 2^34 nonces per GPU"),
-    "4": dict(msg="cmu440", bits=40, scaling="strong",
-              desc="BASELINE configs[3]: 2^40 nonces in total, split evenly over the GPUs"),
-}
+def split(lo, hi, parts, i):
+    """The i-th of `parts` contiguous, near-equal pieces of [lo, hi] (None if empty)."""
+    n = hi - lo + 1
+    a = lo + n * i // parts
+    b = lo + n * (i + 1) // parts - 1
+    return (a, b) if b >= a else None
 
 
-def rank_range(rank, world, bits, scaling):
-    """Weak: rank r scans its own 2^bits shard.  Strong: 2^bits in total,
-    contiguous equal slices."""
-    if scaling == "weak":
-        return shard(rank, bits)
-    total = 1 << bits
-    lo = total * rank // world
-    return lo, total * (rank + 1) // world - 1
+def step_range(cfg, k, steps):
+    """The whole nonce range of step k (all ranks together).  Weak configs scan
+    the same [0, N*2^bits) every step (the caller splits it per GPU); the strong
+    config's K steps are K slices of [0, 2^bits)."""
+    if cfg["scaling"] == "weak":
+        return None
+    return split(0, (1 << cfg["bits"]) - 1, steps, k % steps)
+
+
+def rank_range(cfg, rank, world, k=0, steps=1):
+    """This rank's shard of step k."""
+    if cfg["scaling"] == "weak":
+        return shard(rank, cfg["bits"])
+    return split(*step_range(cfg, k, steps), world, rank)
+
+
+def job_range(cfg, world, k=0, steps=1):
+    """Every rank's shard of step k together."""
+    if cfg["scaling"] == "weak":
+        return 0, (world << cfg["bits"]) - 1
+    return step_range(cfg, k, steps)
 
 
 def merge(results):
@@ -80,40 +125,40 @@ def merge(results):
     return min(results)
 
 
-def gather_merge(r, world, dist, torch, device):
+def host_merge(r, world, dist):
+    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors)."""
     if world == 1:
         return r
-    import numpy as np
-    t = torch.from_numpy(np.array([r[0], r[1]], dtype=np.uint64).view(np.int64)).to(device)
+    import torch
+    t = torch.tensor([r[0] - (1 << 63), r[1] - (1 << 63)], dtype=torch.int64)  # u64 -> i64, order kept
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t)
-    vals = [tuple(int(v) for v in o.cpu().numpy().view(np.uint64)) for o in out]
-    return merge(vals)
+    return merge(tuple(int(v) + (1 << 63) for v in o.tolist()) for o in out)
 
 
-def run_steps(search, lo, hi, steps, warmup, world, dist, torch, device, sync):
-    """Warmup, then exactly `steps` timed searches + merges between barriers.
-    Returns (merged result, this rank's elapsed seconds)."""
-    r = None
-    for _ in range(warmup):
-        r = gather_merge(search(lo, hi), world, dist, torch, device)
-    if world > 1:
-        dist.barrier()
+def run_timed(step, steps, warmup, barrier, sync):
+    """W untimed warmup steps, then exactly `steps` timed steps between a barrier
+    + device sync on both sides.  step(k) returns the merged (hash, nonce) of
+    step k.  Returns (min over the timed steps, this rank's elapsed seconds)."""
+    for w in range(warmup):
+        step(w)
+    barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        r = gather_merge(search(lo, hi), world, dist, torch, device)
-    if world > 1:
-        dist.barrier()
+    best = None
+    for k in range(steps):
+        r = step(k)
+        best = r if best is None else merge([best, r])
+    barrier()
     sync()
-    return r, time.perf_counter() - t0
+    return best, time.perf_counter() - t0
 
 
 def golden_expect(msg, lo, hi):
     """The expected (hash, nonce) of [lo, hi] from the full-size fixtures
-    (tests/golden/fullsize_*.json, scanned with OpenSSL by gen_fullsize.py) when
-    [lo, hi] is a union of their chunks; None otherwise.  Data only: no oracle
-    code runs here."""
+    (tests/golden/fullsize_*.json, scanned on the CPU by gen_fullsize.py /
+    gen_cfg4.py) when [lo, hi] is a union of their chunks; None otherwise.
+    Data only: no oracle code runs here."""
     for path in sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "fullsize_*.json"))):
         with open(path) as f:
             d = json.load(f)
@@ -179,33 +224,44 @@ def cpu_baseline(msg, threads):
     }
 
 
-def dominant_piece(msg, lo, hi, dom):
-    """The largest launch of the dominant fast_search<J, MODE> in this search's own plan."""
+def largest_piece(msg, lo, hi, var):
+    """The largest launch of fast_search<word, mode> in the plan of [lo, hi]."""
     import minehip
     ps = [p for p in minehip.plan(msg, lo, hi)
-          if p["kind"] == 0 and p["word"] == dom.get("word") and p["mode"] == dom.get("mode")]
+          if p["kind"] == 0 and p["word"] == var["word"] and p["mode"] == var["mode"]]
     return max(ps, key=lambda p: p["count"]) if ps else None
 
 
-def pmc_counters(msg, piece, dev, timeout=90):
-    """PMC counters of ONE launch of the dominant kernel: three separate rocprofv3
-    --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ_INSTS_VALU + GRBM_GUI_ACTIVE -- the
-    first two do not fit one pass) over a child process (tools/pmc_launch.py) that
-    searches exactly that launch's nonces.  Returns (values, error): values maps
-    each counter to its per-dispatch sum, plus "dur_ns" from the last pass."""
+# rocprofv3 --pmc passes: one block-limited counter set per run
+# (MI355X_MICROARCH.md: 8 SQ, 4 TCC -- FETCH_SIZE takes 3, WRITE_SIZE 2 --, 2 GRBM).
+PMC_PASSES = (
+    ("FETCH_SIZE",),
+    ("WRITE_SIZE",),
+    ("GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+     "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"),
+    ("GRBM_GUI_ACTIVE", "SQ_ACTIVE_INST_ANY", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU",
+     "SQ_ACTIVE_INST_SCA", "SQ_INSTS_VALU_INT32", "SQ_IFETCH", "SQ_BUSY_CU_CYCLES", "SQ_CYCLES"),
+)
+
+
+def pmc_counters(msg, pieces, dev, timeout=90, passes=PMC_PASSES):
+    """PMC counters of ONE launch of each given piece: one rocprofv3 --pmc run
+    per counter set over a child process (tools/pmc_launch.py) that searches
+    exactly those launches' nonces.  Returns ({kernel name: {counter: value,
+    "dur_ns": ..., "cycles": ...}}, error)."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"
-    name = f"fast_search<{piece['word']}, {piece['mode']}>"
-    lo, hi = piece["first"], piece["first"] + piece["count"] - 1
-    vals = {}
+    names = [f"fast_search<{p['word']}, {p['mode']}>" for p in pieces]
+    ranges = [f"{p['first']}:{p['first'] + p['count'] - 1}" for p in pieces]
+    vals = {n: {} for n in names}
     work = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     try:
-        for counters in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "GRBM_GUI_ACTIVE"]):
-            out = os.path.join(work, counters[0])
+        for counters in passes:
+            out = os.path.join(work, f"p{passes.index(counters)}")
             cmd = [prof, "--pmc", *counters, "-d", out, "-o", "run", "--output-format", "csv", "--",
-                   sys.executable, os.path.join(ROOT, "tools", "pmc_launch.py"), msg, str(lo), str(hi), str(dev)]
+                   sys.executable, os.path.join(ROOT, "tools", "pmc_launch.py"), msg, str(dev), *ranges]
             try:
                 rc = subprocess.run(cmd, cwd="/tmp", env=env, timeout=timeout, stdout=subprocess.DEVNULL,
                                     stderr=subprocess.PIPE).returncode
@@ -216,16 +272,58 @@ def pmc_counters(msg, piece, dev, timeout=90):
                 return None, f"rocprofv3 --pmc {' '.join(counters)} failed (rc {rc})"
             per = {}
             for r in csv.DictReader(open(files[0])):
-                if name in r["Kernel_Name"] and r["Counter_Name"] in counters:
-                    d = per.setdefault(r["Dispatch_Id"], {})
-                    d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-                    d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            if len(per) != 1:
-                return None, f"{len(per)} {name} dispatches in the --pmc {' '.join(counters)} pass, expected 1"
-            vals.update(next(iter(per.values())))
+                name = next((n for n in names if n in r["Kernel_Name"]), None)
+                if name is None or r["Counter_Name"] not in counters:
+                    continue
+                d = per.setdefault((name, r["Dispatch_Id"]), {})
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            for n in names:
+                ds = [v for (k, _), v in per.items() if k == n]
+                if len(ds) != 1:
+                    return None, f"{len(ds)} {n} dispatches in the --pmc {' '.join(counters)} pass, expected 1"
+                if "GRBM_GUI_ACTIVE" in ds[0]:  # per-pass clock, kept per pass
+                    ds[0][f"GRBM_GUI_ACTIVE@{passes.index(counters)}"] = ds[0].pop("GRBM_GUI_ACTIVE")
+                    ds[0][f"dur_ns@{passes.index(counters)}"] = ds[0]["dur_ns"]
+                vals[n].update(ds[0])
     finally:
         shutil.rmtree(work, ignore_errors=True)
     return vals, None
+
+
+def pmc_derived(v, piece, cus):
+    """Per-launch PMC figures of one fast_search launch (raw counters kept).
+    SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* count quad-cycles summed over
+    waves; GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md)."""
+    g, dur = v["GRBM_GUI_ACTIVE@2"], v["dur_ns@2"]
+    cycles = g / 8                       # shader clocks the launch took
+    simds = cus * 4
+    nonces = piece["count"]
+    wc = v["SQ_WAVE_CYCLES"]
+    out = {
+        "sclk_ghz": round(cycles / dur, 3),
+        "pmc_launch_ms": round(dur / 1e6, 3),
+        "nonces": nonces,
+        "valu_instr_per_nonce": round(v["SQ_INSTS_VALU"] * 64 / nonces, 1),
+        # SIMD cycles per issued wave64 VALU instruction (2 = every issue slot used)
+        "cycles_per_valu_instr": round(cycles * simds / v["SQ_INSTS_VALU"], 3),
+        # mean resident waves per SIMD over the launch (occupancy)
+        "waves_per_simd": round(wc * 4 / (cycles * simds), 2),
+        "waves": int(v["SQ_WAVES"]),
+        # share of wave lifetime: issuing VALU / stalled on issue / parked on a wait
+        "valu_active_of_wave_cycles": round(v["SQ_ACTIVE_INST_VALU"] / wc, 4),
+        "wait_inst_any_of_wave_cycles": round(v["SQ_WAIT_INST_ANY"] / wc, 4),
+        "wait_any_of_wave_cycles": round(v["SQ_WAIT_ANY"] / wc, 4),
+        # VALU busy per SIMD (rocprof's VALUBusy: ACTIVE_INST_VALU x 4 quad->cycles / SIMD-cycles)
+        "valu_busy": round(v["SQ_ACTIVE_INST_VALU"] * 4 / (cycles * simds), 4),
+        # quad-cycles in which a SIMD issued two VALU instructions, per SIMD quad-cycle
+        "valu2_of_simd_quads": round(v["SQ_ACTIVE_INST_VALU2"] / (cycles * simds / 4), 4),
+        "counters": {k: v[k] for k in sorted(v) if not k.startswith("dur_ns")},
+    }
+    if "GRBM_GUI_ACTIVE@3" in v:
+        out["sclk_ghz_pass4"] = round(v["GRBM_GUI_ACTIVE@3"] / 8 / v["dur_ns@3"], 3)
+        out["salu_instr_per_nonce"] = round(v["SQ_INSTS_SALU"] * 64 / nonces, 2)
+    return out
 
 
 def gpu_config1(search_dev):
@@ -239,20 +337,88 @@ def gpu_config1(search_dev):
     return {"config1_ms": round(sorted(ts)[5] * 1e3, 3), "config1_result": list(r)}
 
 
+def die(msg, code=2):
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def kernel_totals(per_dev_kstats):
+    """Sum the per-variant HIP-event stats over devices; largest time first."""
+    tot = {}
+    for ks in per_dev_kstats:
+        for k in ks:
+            t = tot.setdefault(k["name"], dict(k, launches=0, nonces=0, ns=0, ops=0, slots=0))
+            for f in ("launches", "nonces", "ns", "ops", "slots"):
+                t[f] += k[f]
+    return sorted(tot.values(), key=lambda k: -k["ns"])
+
+
+def roofline(kst, cus, n_devices):
+    """Roofline of the dominant kernel from its HIP-event launch times (summed
+    over devices, so achieved is per GPU).  frac is on SURVEY §8(d) D4's
+    algorithmic basis; slot_util counts the issue slots of the compiled loop."""
+    peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
+    if not kst:
+        return {"bound": "valu", "achieved": None, "peak": round(peak, 3), "frac": None}
+    dom = kst[0]
+    blocks = 1 if dom["mode"] == 0 else 2       # tail blocks hashed per nonce (Pre/Two: 2)
+    sec = dom["ns"] * 1e-9
+    ghs = dom["nonces"] / sec / 1e9
+    alg = dom["nonces"] * SURVEY_OPS_PER_COMPRESSION * blocks  # int32 ops, §8(d) D4
+    achieved = alg / sec / 1e12
+    slots = dom["slots"] / sec / 1e12           # lane issue slots (one nonce = one lane)
+    launches = max(1, dom["launches"])
+    line = {
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": round(peak, 3),
+        "unit": "T int32 VALU ops/s per GPU",
+        "frac": round(achieved / peak, 4),
+        "frac_alg": round(achieved / peak, 4),
+        "basis": f"SURVEY §8(d) D4: {SURVEY_OPS_PER_COMPRESSION} ops per compression x {blocks} tail block(s) "
+                 f"per nonce over the dominant kernel's HIP-event launch time; peak {cus} CU x "
+                 f"{LANES_PER_CU_CLK} lanes/clk x {PEAK_SCLK_HZ / 1e9} GHz",
+        "kernel": dom["name"],
+        "tail_blocks": blocks,
+        "launches": dom["launches"],
+        "devices": n_devices,
+        "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),
+        "nonces_per_launch": dom["nonces"] // launches,
+        "alg_ops_per_launch": alg // launches,
+        "kernel_ghs": round(ghs, 4),
+        "slot_util": {
+            "achieved": round(slots, 3), "peak": round(peak, 3), "frac": round(slots / peak, 4),
+            "slots_per_nonce": round(dom["slots"] / max(1, dom["nonces"]), 1),
+            "instr_per_nonce": round(dom["ops"] / max(1, dom["nonces"]), 1),
+            "note": "issue slots of the compiled per-nonce loop (full-rate op 1, half-rate v_alignbit/"
+                    "v_add3 2; DESIGN.md §4), hoisted run/group work excluded"},
+        "full_compression_instr": OPS_PER_BLOCK,
+    }
+    if len(kst) > 1:
+        s = kst[1]
+        line["second_kernel"] = {"kernel": s["name"], "ms": round(s["ns"] / 1e6, 3),
+                                 "kernel_ghs": round(s["nonces"] / (s["ns"] * 1e-9) / 1e9, 4),
+                                 "instr_per_nonce": round(s["ops"] / max(1, s["nonces"]), 1)}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="workload (default: configs[1] '2' at N = 1, configs[3] '4' at N > 1)")
     ap.add_argument("--msg", default=None, help="override the config's message")
     ap.add_argument("--bits", type=int, default=None, help="override log2 nonces per GPU (weak) / total (strong)")
+    ap.add_argument("--multi", action="store_true", help="N = 1 through mh_search_multi (the in-process path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes behind roofline.traffic")
-    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="backend of the 16-byte merge and the timing max (nccl = RCCL on ROCm)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     args = ap.parse_args()
-    cfg = dict(CONFIGS[args.config])
+    if args.gpus < 1 or args.steps < 1 or args.warmup < 0:
+        die("--gpus and --steps must be >= 1, --warmup >= 0")
+    cfg_name = args.config or default_config(args.gpus)
+    cfg = dict(CONFIGS[cfg_name])
     if args.msg is not None:
         cfg["msg"] = args.msg
     if args.bits is not None:
@@ -261,114 +427,147 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # test-only: run every rank on one device (rehearsing N>1 on a 1-GPU box; gloo only,
-    # RCCL refuses two ranks on one GPU)
+    launched = world > 1
+    if launched and world != args.gpus:
+        die(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch one process per GPU or none")
+    # test-only: every rank on one device (rehearsing N > 1 on a 1-GPU box)
     if os.environ.get("BENCH_DEVICE") is not None:
         local = int(os.environ["BENCH_DEVICE"])
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
+    # torch first: its HIP runtime must be the one loaded when libminehip's
+    # dependency is resolved (the library then shares it).  device_count()
+    # does not initialise the GPU.
     import torch
-    dist = None
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    comm_device = device if args.dist_backend == "nccl" else torch.device("cpu")
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
-        else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-
+    ndev = torch.cuda.device_count()
+    if launched:
+        if local >= ndev:
+            die(f"rank {rank}: HIP device {local} not visible ({ndev} visible)")
+        devs = [local]
+    else:
+        if ndev < args.gpus:
+            die(f"--gpus {args.gpus} but {ndev} HIP device(s) visible")
+        devs = list(range(args.gpus))
+    torch.cuda.set_device(devs[0])
     import minehip
-    if minehip.device_count() <= local:
-        raise RuntimeError(f"rank {rank}: no HIP device {local}")
+    if minehip.device_count() != ndev:
+        die(f"libminehip sees {minehip.device_count()} devices, torch {ndev}")
+    dist = None
+    if launched:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # host merge: no RCCL
+
     msg = cfg["msg"].encode()
-    lo, hi = rank_range(rank, world, cfg["bits"], cfg["scaling"])
+    n_gpus = args.gpus
+    steps = args.steps
+    multi = (not launched) and (n_gpus > 1 or args.multi)
+    done = {d: 0 for d in devs}  # nonces searched per device in the timed region
 
-    def search(a, b):
-        return minehip.search(msg, a, b, local)
+    def step(k, timed=False):
+        if launched:
+            rr = rank_range(cfg, rank, world, k, steps)
+            r = minehip.search(msg, rr[0], rr[1], devs[0]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
+            if timed and rr:
+                done[devs[0]] += rr[1] - rr[0] + 1
+            return host_merge(r, world, dist)
+        lo, hi = job_range(cfg, n_gpus, k, steps)
+        if multi:
+            return minehip.search_multi(msg, lo, hi, devs)
+        return minehip.search(msg, lo, hi, devs[0])
 
-    # warmup: W untimed steps, each a search plus the 16-byte merge, so that the
-    # collective's first-use setup (RCCL channels / gloo pairs) stays out of the timed region
-    for _ in range(args.warmup):
-        gather_merge(search(lo, hi), world, dist, torch, comm_device)
-    if world > 1:
-        warm = torch.zeros(1, dtype=torch.float64, device=comm_device)
-        dist.all_reduce(warm, op=dist.ReduceOp.MAX)  # the timing max below uses it too
-        if args.warmup == 0:
-            gather_merge((0, 0), world, dist, torch, comm_device)
-    minehip.profile_enable(local, True)
-    r, elapsed = run_steps(search, lo, hi, args.steps, 0, world, dist, torch, comm_device, torch.cuda.synchronize)
-    prof = minehip.profile_read(local)
-    kstats = minehip.profile_kernels(local)  # per fast_search<J, MODE>, largest time first
-    minehip.profile_enable(local, False)
+    barrier = (lambda: dist.barrier()) if launched else (lambda: None)
+    for w in range(args.warmup):
+        step(w)
+    for d in devs:
+        minehip.profile_enable(d, True)
+    r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize)
+    per_dev = []
+    for d in devs:
+        pr = minehip.profile_read(d)
+        per_dev.append({"dev": d, "rank": rank, "prof": pr, "kstats": minehip.profile_kernels(d)})
+        minehip.profile_enable(d, False)
+    for p in per_dev:
+        p["nonces"] = done[p["dev"]] if launched else p["prof"]["fast_nonces"] + p["prof"]["generic_nonces"]
+        p["elapsed"] = elapsed
 
     t_max = elapsed
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_device)
+    if launched:
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_dev)
+        per_dev = [p for g in gathered for p in g]
 
-    total = (1 << cfg["bits"]) * (world if cfg["scaling"] == "weak" else 1)
-    nonces = total * args.steps
-    value = nonces / t_max / 1e9
-    props = torch.cuda.get_device_properties(device)
+    if cfg["scaling"] == "weak":
+        total = (1 << cfg["bits"]) * n_gpus * steps
+        step_nonces = (1 << cfg["bits"]) * n_gpus
+    else:
+        total = 1 << cfg["bits"]
+        step_nonces = total // steps
+    value = total / t_max / 1e9
+    props = torch.cuda.get_device_properties(devs[0])
     cus = int(props.multi_processor_count)
-    peak = cus * SLOT_LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
-    instr_peak = cus * INSTR_LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
-    # algorithmic lane-instructions: sum over fast launches of nonces x nonce_ops (x 64 lanes / 64 nonces)
-    # dominant kernel: the fast_search<J, MODE> variant with the most time.  Its
-    # algorithmic work per launch = nonces x nonce_ops (lane-instructions), over
-    # its average HIP-event launch duration.
-    dom = kstats[0] if kstats else {"name": None, "launches": 0, "nonces": 0, "ns": 0, "ops": 0, "slots": 0}
-    launches = max(1, dom["launches"])
-    achieved = dom["slots"] / (dom["ns"] * 1e-9) / 1e12 if dom["ns"] else 0.0
-    instr_achieved = dom["ops"] / (dom["ns"] * 1e-9) / 1e12 if dom["ns"] else 0.0
-    all_achieved = prof["fast_slots"] / (prof["fast_ns"] * 1e-9) / 1e12 if prof["fast_ns"] else 0.0
-
-    traffic, traffic_note, alg_bytes, pmc = None, "not measured (N > 1 or --no-pmc)", None, None
-    piece = dominant_piece(msg, lo, hi, dom) if dom["name"] else None
-    if piece is not None:
-        runs = piece["count"] // 10 ** piece["lo_digits"]
-        alg_bytes = -(-runs // 256) * 16  # one 16-byte (hash, nonce) partial per 256-lane workgroup
-    if rank == 0 and world == 1 and not args.no_pmc and piece is not None:
-        vals, err = pmc_counters(cfg["msg"], piece, local)
+    kst = kernel_totals([p["kstats"] for p in per_dev])
+    roof = roofline(kst, cus, len(per_dev))
+    # algorithmic bytes of the dominant launch: one 16-byte (hash, nonce) partial per 256-lane workgroup
+    job_lo, job_hi = job_range(cfg, n_gpus, 0, 1 if cfg["scaling"] == "weak" else steps)
+    my_lo, my_hi = (rank_range(cfg, rank, world, 0, steps) if launched else (job_lo, job_hi))
+    pieces = []
+    for var in kst[:2]:
+        p = largest_piece(msg, my_lo, my_hi, var)
+        if p is not None:
+            pieces.append(p)
+    if pieces:
+        p = pieces[0]
+        roof["algorithmic_bytes_per_launch"] = -(-(p["count"] // 10 ** p["lo_digits"]) // 256) * 16
+    roof["traffic"] = None
+    roof["traffic_note"] = "not measured (N > 1 or --no-pmc)"
+    if rank == 0 and n_gpus == 1 and not args.no_pmc and pieces:
+        vals, err = pmc_counters(cfg["msg"], pieces, devs[0])
         if vals is None:
-            traffic_note = err
+            roof["traffic_note"] = err
         else:
+            v0 = vals[f"fast_search<{pieces[0]['word']}, {pieces[0]['mode']}>"]
             # HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB, the 2x being gfx950's wide-read
             # correction (MI355X_MICROARCH.md, HBM section)
-            traffic = int((2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024)
-            traffic_note = (f"FETCH_SIZE {vals['FETCH_SIZE']:.2f} KiB (x2 gfx950 correction), "
-                            f"WRITE_SIZE {vals['WRITE_SIZE']:.2f} KiB")
-            # clock the launch actually ran at: GRBM_GUI_ACTIVE is summed over the 8 XCDs
-            sclk = vals["GRBM_GUI_ACTIVE"] / 8 / vals["dur_ns"]
-            pmc = {"sclk_ghz": round(sclk, 3),
-                   "valu_instr_per_nonce": round(vals["SQ_INSTS_VALU"] * 64 / piece["count"], 1),
-                   "pmc_launch_ms": round(vals["dur_ns"] / 1e6, 3),
-                   "frac_at_sclk": round(achieved / (cus * SLOT_LANES_PER_CU_CLK * sclk * 1e9 / 1e12), 4),
-                   "note": "one launch of the dominant kernel under rocprofv3 --pmc SQ_INSTS_VALU "
-                           "GRBM_GUI_ACTIVE; frac_at_sclk = achieved / (CUs x 128 x sclk)"}
+            roof["traffic"] = int((2 * v0["FETCH_SIZE"] + v0["WRITE_SIZE"]) * 1024)
+            roof["traffic_unit"] = "bytes per launch (HBM, PMC)"
+            roof["traffic_note"] = (f"FETCH_SIZE {v0['FETCH_SIZE']:.2f} KiB (x2 gfx950 correction), "
+                                    f"WRITE_SIZE {v0['WRITE_SIZE']:.2f} KiB")
+            roof["pmc"] = pmc_derived(v0, pieces[0], cus)
+            roof["pmc"]["kernel"] = kst[0]["name"]
+            # achieved / frac again at the clock this launch ran at
+            at = roof["pmc"]["sclk_ghz"] * 1e9
+            roof["pmc"]["frac_alg_at_sclk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+            roof["pmc"]["slot_util_at_sclk"] = round(roof["slot_util"]["achieved"]
+                                                     / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+            if len(pieces) > 1:
+                v1 = vals[f"fast_search<{pieces[1]['word']}, {pieces[1]['mode']}>"]
+                roof["second_kernel"]["pmc"] = pmc_derived(v1, pieces[1], cus)
 
     if rank == 0:
-        # the merged range of this run: every rank's shard
-        m_lo = min(rank_range(q, world, cfg["bits"], cfg["scaling"])[0] for q in range(world))
-        m_hi = max(rank_range(q, world, cfg["bits"], cfg["scaling"])[1] for q in range(world))
+        # the merged range of the timed region
+        m_lo = job_range(cfg, n_gpus, 0, steps)[0]
+        m_hi = job_range(cfg, n_gpus, steps - 1, steps)[1]
         expect = golden_expect(msg, m_lo, m_hi)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if n_gpus == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cfg["msg"], threads)
-            cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, local))
+            cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, devs[0]))
+        per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
+                       "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
+                       "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
+                       if p["kstats"] and p["kstats"][0]["ns"] else None}
+                      for p in per_dev]
         line = {
             "metric": METRIC,
             "value": round(value, 4),
             "unit": "GH/s",
-            "n_gpus": world,
-            "steps": args.steps,
+            "n_gpus": n_gpus,
+            "steps": steps,
             "warmup": args.warmup,
-            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "ms_per_step": round(t_max / steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,
@@ -376,51 +575,29 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": cfg["desc"],
+                "config": cfg_name,
                 "msg": cfg["msg"] if len(cfg["msg"]) <= 16 else f"{cfg['msg'][:1]!r} x {len(cfg['msg'])}",
-                "nonces_per_step": total,
-                "nonces_per_gpu": total // world,
-                "parallelism": f"one contiguous shard per GPU x{world}, 16-byte (hash, nonce) merge",
+                "nonces_timed": total,
+                "nonces_per_step": step_nonces,
+                "nonces_per_gpu_per_step": step_nonces // n_gpus,
+                "driver": ("one process per GPU (launcher), gloo host merge" if launched else
+                           "one process, mh_search_multi: one host thread + HIP stream per device" if multi else
+                           "one process, mh_search on one device"),
+                "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved, 3),
-                "peak": round(peak, 3),
-                "unit": "T VALU lane issue-slots/s (int32)",
-                "frac": round(achieved / peak, 4) if peak else None,
-                "traffic": traffic,
-                "traffic_unit": "bytes per launch (HBM, PMC)",
-                "traffic_note": traffic_note,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "pmc": pmc,
-                "kernel": dom["name"],
-                "launches": dom["launches"],
-                "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),
-                "slots_per_launch": dom["slots"] // launches,
-                "slots_per_nonce": round(dom["slots"] / max(1, dom["nonces"]), 1),
-                "kernel_ghs": round(dom["nonces"] / (dom["ns"] * 1e-9) / 1e9, 4) if dom["ns"] else None,
-                "peak_basis": f"{cus} CU x {SLOT_LANES_PER_CU_CLK} lane-slots/clk x {PEAK_SCLK_HZ / 1e9} GHz",
-                "instruction_issue": {
-                    "achieved": round(instr_achieved, 3), "peak": round(instr_peak, 3),
-                    "frac": round(instr_achieved / instr_peak, 4),
-                    "instr_per_nonce": round(dom["ops"] / max(1, dom["nonces"]), 1),
-                    "note": "a stream mixing half-rate ops issues ~64 lanes/clk/CU whatever the mix "
-                            "(tools/gen_valu_mix.py): this is the practical ceiling, the slot peak the hardware one"},
-                "full_compression_instr": OPS_PER_BLOCK,
-                "all_fast_kernels": {"achieved": round(all_achieved, 3), "launches": prof["fast_launches"],
-                                     "ms": round(prof["fast_ns"] / 1e6, 3),
-                                     "slots_per_nonce": round(prof["fast_slots"] / max(1, prof["fast_nonces"]), 1)},
-            },
+            "per_device": per_device,
+            "roofline": roof,
             "cpu_baseline": cpu,
             # self-check on the product path: the winning nonce re-hashed by the
             # generic kernel (mh_hash_batch), not the fast kernel that found it
             "result": {"hash": r[0], "nonce": r[1],
-                       "rehash_ok": minehip.Hash(msg, r[1], local) == r[0],
+                       "rehash_ok": minehip.Hash(msg, r[1], devs[0]) == r[0],
                        "range": [m_lo, m_hi],
                        # bit-exact against the full-size fixture when one covers the range
                        "golden_ok": None if expect is None else tuple(r) == expect},
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if launched:
         dist.barrier()
         dist.destroy_process_group()
 

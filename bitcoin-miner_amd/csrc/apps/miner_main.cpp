@@ -77,8 +77,11 @@ int run_lsp(const char* hostport, const std::vector<int>& devs) {
         size_t on = 0;
         const int hr = mh_miner_handle(devs.data(), (int)devs.size(), (const char*)buf.data(), n, out, sizeof out,
                                        &on);
-        if (hr == MH_EINVAL || hr == MH_ERANGE) continue;  // not a Request
-        if (hr != MH_OK) {  // a GPU failure: leave, so the server reassigns the chunk
+        if (hr == MH_ENOTREQ || hr == MH_ERANGE) {  // not a Request, or Lower > Upper: no answer
+            fprintf(stderr, "minehip-miner: ignored a message: %s\n", mh_last_error());
+            continue;
+        }
+        if (hr != MH_OK) {  // the search failed: leave, so the server reassigns the chunk
             fprintf(stderr, "minehip-miner: %s\n", mh_last_error());
             status = 1;
             break;

@@ -58,7 +58,12 @@ int main(int argc, char** argv) {
             continue;
         }
         if (r == LSP_OK) {
-            mh_server_read(v, conn, (const char*)buf.data(), n, now);  // bad payloads are ignored
+            // a refused Request gets no Result: close that client, which then prints
+            // Disconnected; other bad payloads are ignored
+            if (mh_server_read(v, conn, (const char*)buf.data(), n, now) == MH_EREJECTED) {
+                fprintf(stderr, "minehip-server: conn %d: %s\n", conn, mh_last_error());
+                lsp_server_close_conn(s, conn);
+            }
         } else if (conn != 0) {  // a client or miner lost / closed (server_api.go:7-17)
             mh_server_lost(v, conn, now);
             mh_sched_stats st;

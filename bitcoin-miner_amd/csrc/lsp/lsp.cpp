@@ -41,6 +41,7 @@ namespace lsp440 {
 namespace {
 
 enum MsgType { kConnect = 0, kData = 1, kAck = 2 };
+constexpr size_t kMaxDatagram = LSP_MAX_DATAGRAM;
 
 struct Wire {
     int type = 0;
@@ -400,6 +401,7 @@ class Endpoint {
                 if (e.rc == LSP_OK && !e.payload.empty()) memcpy(buf, e.payload.data(), e.payload.size());
                 rc = e.rc;
                 if (!server_ && rc != LSP_OK) sticky_ = rc;
+                if (server_ && rc != LSP_OK) forget(e.conn, rc);  // the caller now knows: free the Conn
                 events_.pop_front();
             }
         } else if (!server_ && sticky_ != LSP_OK) {
@@ -419,7 +421,10 @@ class Endpoint {
         Conn* c = nullptr;
         if (server_) {
             auto it = conns_.find(conn);
-            if (it == conns_.end()) return LSP_EINVAL;
+            if (it == conns_.end()) {
+                auto g = gone_.find(conn);
+                return g == gone_.end() ? LSP_EINVAL : g->second;
+            }
             c = &it->second;
             if (closing_all_) return LSP_ECLOSED;
         } else {
@@ -427,6 +432,7 @@ class Endpoint {
         }
         if (c->lost) return LSP_ELOST;
         if (c->done || c->closing) return LSP_ECLOSED;
+        if (frame_size(*c, n) > kMaxDatagram) return LSP_ETOOBIG;  // could never be delivered
         c->unsent.emplace_back(c->next_seq++, std::string((const char*)p, n));
         pump(*c);
         return LSP_OK;
@@ -435,7 +441,8 @@ class Endpoint {
     int close_conn(int conn) {
         std::lock_guard<std::mutex> lk(mu_);
         auto it = conns_.find(conn);
-        if (it == conns_.end() || it->second.done) return LSP_EINVAL;
+        if (it == conns_.end()) return gone_.count(conn) ? LSP_ECLOSED : LSP_EINVAL;
+        if (it->second.done) return LSP_EINVAL;
         it->second.closing = true;
         maybe_finish(it->second);
         return LSP_OK;
@@ -491,6 +498,7 @@ class Endpoint {
     std::deque<Event> events_;
     Conn cli_;                   // client side: the one connection
     std::map<int, Conn> conns_;  // server side, by connID
+    std::map<int, int> gone_;    // server side: connIDs whose end Read reported -> LSP_ELOST / LSP_ECLOSED
     std::map<uint64_t, int> by_addr_;
     int next_id_ = 1;
 
@@ -507,6 +515,27 @@ class Endpoint {
     void wake() {
         const uint64_t one = 1;
         if (wake_ >= 0) (void)!::write(wake_, &one, sizeof one);
+    }
+
+    // Bytes of the Data datagram that would carry an n-byte payload on c.
+    size_t frame_size(const Conn& c, size_t n) const {
+        Wire w;
+        w.type = kData;
+        w.conn = c.id;
+        w.seq = c.next_seq;
+        w.size = (int64_t)n;
+        w.has_payload = true;
+        w.payload.assign(n, '\0');
+        return marshal(w).size();
+    }
+
+    // A server connection whose terminal event the caller has read: drop its
+    // buffers, remember only how it ended (for later write / close_conn).
+    void forget(int id, int rc) {
+        auto it = conns_.find(id);
+        if (it == conns_.end() || !it->second.done) return;
+        gone_[id] = rc;
+        conns_.erase(it);
     }
 
     // -- datagrams out (mu_ held) --

@@ -385,8 +385,8 @@ int mh_miner_handle(const int* devs, int ndev, const char* request, size_t len, 
                     size_t* out_len) {
     if (!request || !devs || ndev <= 0) return mh::set_error(MH_EINVAL, "bad arguments");
     Msg m;
-    if (!decode(request, len, &m)) return mh::set_error(MH_EINVAL, "payload is not a JSON bitcoin.Message");
-    if (m.type != 1) return mh::set_error(MH_EINVAL, "not a Request");  // message.go:10
+    if (!decode(request, len, &m)) return mh::set_error(MH_ENOTREQ, "payload is not a JSON bitcoin.Message");
+    if (m.type != 1) return mh::set_error(MH_ENOTREQ, "not a Request");  // message.go:10
     if (m.lower > m.upper) return mh::set_error(MH_ERANGE, "lower > upper");
     uint64_t h = 0, n = 0;
     const int rc = (ndev == 1)

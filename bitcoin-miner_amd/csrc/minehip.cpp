@@ -170,14 +170,14 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
         // partials buffer holds one slot per block
         if (p.fa.n_runs == 0 || p.fa.L < 1 || p.fa.L > 5 || p.fa.n_hi + p.fa.L > 20)
-            return fail(MH_EINVAL, "internal: bad fast piece");
+            return fail(MH_EINTERNAL, "internal: bad fast piece");
         blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
     } else {
         if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
-            return fail(MH_EINVAL, "internal: bad generic piece");
+            return fail(MH_EINTERNAL, "internal: bad generic piece");
         blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
     }
-    if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINVAL, "internal: grid too large");
+    if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
     if (c->poff + blocks > mh::kMaxBlocksPerLaunch) {
         const int rc = flush_partials(c);
         if (rc) return rc;
@@ -317,9 +317,13 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
         if (devs[i] < 0 || devs[i] >= n) return fail(n <= 0 ? MH_ENODEV : MH_EINVAL, "device index out of range");
     mh::Prefix pre;
     mh::absorb_prefix(msg, len, &pre);
+    // One device and adaptive chunks: nothing to balance, so one search (one
+    // plan, full-size launches) instead of a chain of shrinking chunks.
+    if (ndev == 1 && chunk == 0 && getenv("MINEHIP_TEST_FAIL_WORKER") == nullptr)
+        return search_impl(devs[0], pre, lower, upper, out_hash, out_nonce);
     // One miner per listed device, fed by the server's scheduler (sched.hpp):
-    // chunks sized from each device's measured rate (~100 ms of work, >= 2^26
-    // nonces so the per-chunk launch + sync overhead of ~0.1 ms stays < 1%),
+    // chunks sized from each device's measured rate (~200 ms of work, >= 2^28
+    // nonces so the per-chunk plan + launch tail + sync stays well under 1%),
     // capped at a fair share of what is left so the tail is spread over all
     // devices.  A device that fails hands its chunk back to the others.
     mh_sched_opts o;
@@ -327,12 +331,13 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     if (chunk) {
         o.init_chunk = o.min_chunk = o.max_chunk = chunk;
     } else {
-        o.min_chunk = 1ull << 26;
-        o.target_ns = 100000000ull;
+        o.init_chunk = 1ull << 32;
+        o.min_chunk = 1ull << 28;
+        o.target_ns = 200000000ull;
     }
     mh::Scheduler sched(o);
     for (int i = 0; i < ndev; ++i) sched.add_miner(i);
-    if (sched.submit(0, msg, len, lower, upper) < 0) return fail(MH_EINVAL, "internal: submit failed");
+    if (sched.submit(0, msg, len, lower, upper) < 0) return fail(MH_EINTERNAL, "internal: submit failed");
     std::mutex mu;
     std::condition_variable cv;
     uint64_t gen = 0;  // bumped on every completion or device loss

@@ -52,10 +52,13 @@ void Scheduler::erase_job(int64_t id) {
     }
 }
 
-// rate x target, capped at the job's fair share of what is left, clamped.
+// rate x target, capped at the job's fair share of what is left (guided
+// self-scheduling: half of an even split, so the tail is spread over every
+// miner; a lone miner has no tail to share), clamped.
 uint64_t Scheduler::chunk_size(const Miner& m, const Job& j) const {
     double want = m.rate > 0.0 ? m.rate * (double)o_.target_ns : (double)o_.init_chunk;
-    const u128 share = j.pending() / (u128)(2u * std::max<size_t>(1, miners_.size()));
+    const size_t nm = miners_.size();
+    const u128 share = j.pending() / (u128)(nm > 1 ? 2u * nm : 1u);
     if ((double)share < want) want = (double)share;
     if (want < (double)o_.min_chunk) want = (double)o_.min_chunk;
     if (want > (double)o_.max_chunk) want = (double)o_.max_chunk;

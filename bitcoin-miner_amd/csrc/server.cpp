@@ -73,7 +73,9 @@ int mh_server_read(mh_server* v, int64_t conn, const char* payload, size_t len, 
             break;
         case 1: {  // Request from a client
             const int64_t id = v->s.submit(conn, (const uint8_t*)m.data.data(), m.data.size(), m.lower, m.upper);
-            if (id < 0) rc = (int)id;
+            if (id < 0)  // nothing will ever answer it: the transport closes the client (Disconnected)
+                rc = mh::set_error(MH_EREJECTED, id == MH_ERANGE ? "Request refused: Lower > Upper"
+                                                                 : "Request refused: Data too long");
             break;
         }
         case 2: {  // Result from a miner

@@ -19,6 +19,7 @@ import numpy as np
 
 from ._lib import lib, mh_piece, mh_message, mh_kernel_stat, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
 from ._lib import MH_OK, MH_EINVAL, MH_ERANGE, MH_ETOOLONG, MH_ENODEV, MH_EHIP  # noqa: F401
+from ._lib import MH_ENOTREQ, MH_EINTERNAL, MH_EREJECTED  # noqa: F401
 
 U64_MAX = (1 << 64) - 1
 
@@ -274,7 +275,7 @@ class Server:
         self._h = lib.mh_server_create(ctypes.byref(_opts(**opts)))
         if not self._h:
             _check(MH_EINVAL)
-        self._buf = ctypes.create_string_buffer(MAX_MSG + 256)
+        self._buf = ctypes.create_string_buffer(4096)  # grown on demand (writes())
 
     def close(self):
         if self._h:
@@ -295,10 +296,15 @@ class Server:
         out = []
         conn = ctypes.c_int64()
         n = ctypes.c_size_t()
-        while _chk_neg(lib.mh_server_pop_write(self._h, ctypes.byref(conn), self._buf, len(self._buf),
-                                               ctypes.byref(n))) == 1:
+        while True:
+            rc = lib.mh_server_pop_write(self._h, ctypes.byref(conn), self._buf, len(self._buf), ctypes.byref(n))
+            if rc == MH_EINVAL and n.value > len(self._buf):
+                # an encoded Request can be ~6x its Data (JSON escapes): grow to the reported size
+                self._buf = ctypes.create_string_buffer(n.value)
+                continue
+            if _chk_neg(rc) != 1:
+                return out
             out.append((conn.value, self._buf.raw[:n.value]))
-        return out
 
     def stats(self):
         return _stats(lib.mh_server_stats, self._h)

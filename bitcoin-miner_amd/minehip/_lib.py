@@ -16,6 +16,9 @@ MH_ERANGE = -2
 MH_ETOOLONG = -3
 MH_ENODEV = -4
 MH_EHIP = -5
+MH_ENOTREQ = -6
+MH_EINTERNAL = -7
+MH_EREJECTED = -8
 OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
 
 #: every symbol include/*.h declares

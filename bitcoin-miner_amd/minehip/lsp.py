@@ -25,6 +25,8 @@ LSP_ETIMEOUT = -13
 LSP_EINVAL = -14
 LSP_ESOCK = -15
 LSP_ESHORT = -16
+LSP_ETOOBIG = -17
+MAX_DATAGRAM = 65507  # LSP_MAX_DATAGRAM (include/lsp440.h)
 
 MsgConnect, MsgData, MsgAck = 0, 1, 2  # lsp/message.go:10-14
 
@@ -73,7 +75,8 @@ lib = _load()
 
 _NAMES = {LSP_ECLOSED: "connection closed", LSP_ELOST: "connection lost",
           LSP_ECONNECT: "can not establish connection", LSP_ETIMEOUT: "timeout",
-          LSP_EINVAL: "invalid argument", LSP_ESOCK: "socket error", LSP_ESHORT: "buffer too small"}
+          LSP_EINVAL: "invalid argument", LSP_ESOCK: "socket error", LSP_ESHORT: "buffer too small",
+          LSP_ETOOBIG: "message too big for one datagram"}
 
 
 class LspError(Exception):

@@ -30,6 +30,9 @@
  * requires and dropped-miner recovery never starts.  Here Read returns
  * (connID, LSP_ELOST) once that client's already-received messages are read.
  *
+ * A server connection whose loss or close Read has reported is freed; later
+ * write / close_conn on its id return LSP_ELOST / LSP_ECLOSED.
+ *
  * Every call is thread-safe; each endpoint runs one background thread.
  * Return codes: 0 ok, negative LSP_E*.  Buffers are caller-owned.
  */
@@ -51,6 +54,16 @@ extern "C" {
 #define LSP_EINVAL -14   /* bad argument / unknown connID                                 */
 #define LSP_ESOCK -15    /* socket / address error                                        */
 #define LSP_ESHORT -16   /* caller's buffer too small; *len = the payload size, kept      */
+#define LSP_ETOOBIG -17  /* write: the Data datagram would exceed LSP_MAX_DATAGRAM        */
+
+/* Largest datagram a write may produce (the UDP/IPv4 payload limit); a larger
+ * frame could never be delivered, so write refuses it with LSP_ETOOBIG
+ * instead of resending it forever.  Interop note: the reference's Go peers
+ * read at most MaxMessageSize = 1000 bytes per datagram (lsp/util.go:16,
+ * lsp/client_impl.go:203), i.e. about 600 bytes of payload after JSON and
+ * base64 framing; frames between 1000 and LSP_MAX_DATAGRAM bytes only reach
+ * liblsp440 peers. */
+#define LSP_MAX_DATAGRAM 65507
 
 typedef struct lsp_params {
     int epoch_limit;  /* Params.EpochLimit  */

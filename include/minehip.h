@@ -45,6 +45,9 @@ extern "C" {
 #define MH_ETOOLONG (-3) /* len(msg) > MH_MAX_MSG_LEN                       */
 #define MH_ENODEV (-4)   /* no HIP device / not gfx950                      */
 #define MH_EHIP (-5)     /* a HIP runtime call failed (see mh_last_error)   */
+#define MH_ENOTREQ (-6)  /* mh_miner_handle: the payload is not a JSON Request */
+#define MH_EINTERNAL (-7) /* a launch-plan invariant failed (a library bug)  */
+#define MH_EREJECTED (-8) /* mh_server_read: a client's Request was refused  */
 
 /* Longest accepted message.  The LSP transport caps a datagram at 1000 bytes
  * (lsp/util.go:16, lsp/client_impl.go:203), i.e. ~600 bytes of Data after
@@ -53,7 +56,7 @@ extern "C" {
 #define MH_MAX_MSG_LEN (1u << 20)
 
 /* ABI version of this header, returned by mh_abi_version(). */
-#define MH_ABI_VERSION 1
+#define MH_ABI_VERSION 2
 
 int mh_abi_version(void);
 
@@ -115,8 +118,11 @@ int mh_msg_decode(const char *json, size_t len, mh_message *out, uint8_t *data, 
 /* One step of the GPU miner (miner.go:33 TODO, spec SURVEY.md §8(a) A2):
  * decode a Request payload, search [Lower, Upper] on the listed devices,
  * encode NewResult(hash, nonce) (message.go:38-44) into out.  The Go miner
- * wraps this between lsp.Client.Read and lsp.Client.Write.  MH_EINVAL when
- * the payload is not a Request. */
+ * wraps this between lsp.Client.Read and lsp.Client.Write.  MH_ENOTREQ when
+ * the payload is not a JSON bitcoin.Message of type Request, MH_ERANGE when
+ * its Lower > Upper: a miner skips those.  Any other error comes from the
+ * search itself (MH_EHIP, MH_EINTERNAL, ...): the miner should exit, so the
+ * server's lost-miner path hands the chunk to another miner. */
 int mh_miner_handle(const int *devs, int ndev, const char *request, size_t len, char *out, size_t cap,
                     size_t *out_len);
 

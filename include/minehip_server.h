@@ -119,7 +119,11 @@ void mh_server_destroy(mh_server *v);
 /* lsp.Server.Read returned (conn, payload, nil).  Join registers a miner,
  * Request submits a job for the client `conn`, Result completes the miner's
  * chunk.  Queues the resulting writes.  MH_EINVAL for a payload that is not a
- * Message, or a Result from a connection with no chunk out. */
+ * Message, or a Result from a connection with no chunk out.  MH_EREJECTED for
+ * a client Request that can never be answered (Lower > Upper, Data longer
+ * than MH_MAX_MSG_LEN): nothing is queued, and the caller should close that
+ * connection (lsp.Server.CloseConn) so the client sees it end instead of
+ * waiting forever for a Result. */
 int mh_server_read(mh_server *v, int64_t conn, const char *payload, size_t len, uint64_t now_ns);
 
 /* lsp.Server.Read returned (conn, nil, err): the connection is lost. */

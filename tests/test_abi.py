@@ -31,7 +31,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version_and_devices():
-    assert minehip.lib.mh_abi_version() == 1
+    assert minehip.lib.mh_abi_version() == 2
     assert minehip.device_count() >= 0
 
 
@@ -193,9 +193,14 @@ def test_message_string():
 
 
 def test_miner_handle_rejects_non_requests():
+    # MH_ENOTREQ / MH_ERANGE are the codes a miner skips; anything else comes from the search
+    # itself and makes the miner exit (INTEGRATION.md miner loop, csrc/apps/miner_main.cpp)
     with pytest.raises(minehip.MinehipError) as e:
         minehip.miner_handle(minehip.marshal(minehip.NewJoin()))
-    assert e.value.code == minehip.MH_EINVAL
+    assert e.value.code == minehip.MH_ENOTREQ
+    with pytest.raises(minehip.MinehipError) as e:
+        minehip.miner_handle(b"not json")
+    assert e.value.code == minehip.MH_ENOTREQ
     with pytest.raises(minehip.MinehipError) as e:
         minehip.miner_handle(minehip.marshal(minehip.NewRequest("x", 9, 1)))
     assert e.value.code == minehip.MH_ERANGE

@@ -126,6 +126,16 @@ def test_cluster_cpu_with_dropped_miner(tmp_path):
     assert "lost" in err  # the server saw the dropped miner through LSP
 
 
+def test_config0_full_range_over_lsp(tmp_path):
+    """BASELINE configs[0]: the CPU miner over LSP on localhost, msg "cmu440", nonces
+    0..9,999,999 in full -- the client prints the answer pinned in SURVEY §8(c) C4 and
+    tests/golden/scan_vectors.json (hashlib), with one of three miners dropping mid-job."""
+    out, err = run_cluster([oracle_miner(), oracle_miner(), oracle_miner(drop_after=1)],
+                           "cmu440", 9_999_999, chunk=500_000, timeout=600, tmp=str(tmp_path))
+    assert out == "Result 1228377698034 1067492", err[-2000:]
+    assert "lost" in err
+
+
 @pytest.mark.gpu
 def test_cluster_gpu_with_killed_miner(gpu, tmp_path):
     # 3 GPU miner processes on the box's one GPU; one is SIGKILLed mid-job.

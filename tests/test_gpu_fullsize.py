@@ -11,13 +11,17 @@ reproduce every one of them:
   cfg3a  "a" x 100 [0, 2^34-1]: configs[2], host-midstate block
   cfg3b  "x" x 60  [0, 2^34-1]: configs[2], two tail blocks
   cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
+  cfg4   "cmu440" [0, 2^40-1]: configs[3] whole, its 256 2^32-chunk minima
+         (tests/golden/gen_cfg4.py: SHA-NI scan, checked against OpenSSL)
 
 Reference semantics: bitcoin/hash.go:13-17 and the scan spec of SURVEY.md
 §8(a) A2 (reference stub bitcoin/miner/miner.go:33).
 """
+import os
+
 import pytest
 
-from conftest import load_golden
+from conftest import GOLDEN, load_golden
 from test_gpu_parity import env
 
 pytestmark = pytest.mark.gpu
@@ -79,6 +83,52 @@ def test_plan_knobs_full_size(gpu):
 
 
 def test_search_multi_full_size(gpu):
-    """The scheduler path (one miner per device, chunked) at 2^34 with two tail blocks."""
+    """The scheduler path (one miner per device, chunked) at 2^34 with two tail blocks; one
+    listed device takes the direct path (a single search), two take the scheduler."""
     msg, lo, hi, _, result, _ = fixture("cfg3b")
     assert gpu.search_multi(msg, lo, hi, devs=[0]) == result
+    assert gpu.search_multi(msg, lo, hi, devs=[0, 0]) == result
+
+
+CFG4_HI = (1 << 40) - 1
+
+
+def _cfg4_checks(gpu, got):
+    """configs[3]'s answer, checked by everything that pins it without a second 2^40 scan."""
+    msg = b"cmu440"
+    assert gpu.Hash(msg, got[1]) == got[0]                # re-hashed by the generic kernel
+    assert 0 <= got[1] <= CFG4_HI
+    whole35 = fixture("cfg2")[4]                          # [0, 2^35-1] is a prefix of the range
+    assert got <= whole35 and (got[1] >= 1 << 35 or got == whole35)
+    d = load_golden("fullsize_cfg4s.json")
+    below = [(h, n) for lo, hi, h, n in d["samples"] if hi <= CFG4_HI]
+    assert below and all(got <= s for s in below)         # no sampled chunk beats it
+    path = os.path.join(GOLDEN, "fullsize_cfg4.json")
+    if os.path.exists(path):                              # the full CPU scan of [0, 2^40-1]
+        f = load_golden("fullsize_cfg4.json")
+        assert (f["lo"], f["hi"]) == (0, CFG4_HI)
+        assert got == tuple(f["result"])
+
+
+def test_config3_full_range(gpu):
+    """BASELINE configs[3] at its stated size on one GPU: "cmu440" over [0, 2^40-1] (~33 s)."""
+    _cfg4_checks(gpu, gpu.search(b"cmu440", 0, CFG4_HI))
+
+
+def test_config3_full_range_multi(gpu):
+    """The same 2^40 range through mh_search_multi with eight worker threads (one host thread +
+    stream each, all on device 0): the scheduler's chunking, fair-share tail and host merge."""
+    _cfg4_checks(gpu, gpu.search_multi(b"cmu440", 0, CFG4_HI, devs=[0] * 8))
+
+
+def test_config3_chunks_against_fixture(gpu):
+    """Eight of configs[3]'s 2^32-nonce chunk minima (first, last, the 10^11 and 10^12 buckets)."""
+    path = os.path.join(GOLDEN, "fullsize_cfg4.json")
+    if not os.path.exists(path):
+        pytest.skip("tests/golden/fullsize_cfg4.json not generated")
+    f = load_golden("fullsize_cfg4.json")
+    size = 1 << f["chunk_bits"]
+    picks = sorted({0, 8, 23, 24, 232, 233, 254, 255})
+    for i in picks:
+        a = f["lo"] + i * size
+        assert gpu.search(b"cmu440", a, a + size - 1) == tuple(f["chunks"][i]), i

@@ -333,7 +333,27 @@ def test_server_read_reports_lost_client_after_its_messages():
     assert [srv.Read(2000)[1] for _ in range(3)] == [b"a", b"b", b"c"]
     c, got, err = srv.Read(3000)
     assert (c, got, err.code) == (cid, None, lsp.LSP_ELOST)
+    # the report freed the connection's state; its id still answers "lost"
     assert srv.Write(cid, b"late").code == lsp.LSP_ELOST
+    assert srv.CloseConn(cid).code == lsp.LSP_ECLOSED
+    srv.Close()
+
+
+def test_oversized_write_fails_instead_of_hanging():
+    # a Data frame larger than one UDP datagram could never be delivered: the
+    # write is refused (LSP_ETOOBIG) and the connection stays usable
+    p = fast(limit=20, millis=50)
+    srv, _ = lsp.NewServer(0, p)
+    cl, _ = lsp.NewClient(f"127.0.0.1:{srv.port}", p)
+    big = b"\x00" * lsp.MAX_DATAGRAM  # base64 grows it by 4/3
+    assert cl.Write(big).code == lsp.LSP_ETOOBIG
+    assert cl.Write(b"\x00" * 40000) is None  # 53 KB frame: still one datagram
+    c, got, err = srv.Read(3000)
+    assert err is None and got == b"\x00" * 40000
+    assert srv.Write(c, big).code == lsp.LSP_ETOOBIG
+    assert srv.Write(c, b"ok") is None
+    assert cl.Read(3000) == (b"ok", None)
+    assert cl.Close() is None
     srv.Close()
 
 

@@ -116,6 +116,12 @@ def test_chunk_size_follows_rate_and_fair_share():
     assert a[3] - a[2] + 1 == 1000 // 4
     b = s2.next(2)
     assert b[3] - b[2] + 1 == 750 // 4
+    # a lone miner has no tail to share: its chunk is not halved
+    s3 = Scheduler(init_chunk=10 ** 6, min_chunk=1, max_chunk=10 ** 9)
+    s3.add_miner(1)
+    s3.submit(0, "m", 0, 999)
+    a = s3.next(1)
+    assert (a[2], a[3]) == (0, 999)
 
 
 def test_lost_miner_chunk_is_reassigned_first():
@@ -352,3 +358,35 @@ def test_server_rejects_bad_payloads():
         v.read(1, b'{"Type":7}')
     v.read(1, b'{"type":0}')                                  # Go: case-insensitive keys
     assert v.stats()["miners"] == 1
+
+
+def test_server_refuses_unanswerable_requests():
+    """A Request that can never get a Result (Lower > Upper, Data over MH_MAX_MSG_LEN) is refused
+    with MH_EREJECTED and queues nothing: the transport then closes that client (minehip-server
+    does; INTEGRATION.md's Go loop calls CloseConn), so it sees Disconnected instead of hanging."""
+    v = Server()
+    v.read(1, minehip.marshal(minehip.NewJoin()))
+    with pytest.raises(MinehipError) as e:
+        v.read(2, minehip.marshal(minehip.NewRequest("x", 9, 1)))
+    assert e.value.code == minehip.MH_EREJECTED
+    with pytest.raises(MinehipError) as e:
+        v.read(3, minehip.marshal(minehip.NewRequest("y" * (minehip.MAX_MSG + 1), 0, 1)))
+    assert e.value.code == minehip.MH_EREJECTED
+    assert v.writes() == [] and v.stats()["jobs"] == 0
+    v.lost(2)                                                  # the closed client: nothing to cancel
+    v.read(4, minehip.marshal(minehip.NewRequest("z", 0, 9)))  # the server still works
+    (c, payload), = v.writes()
+    assert c == 1 and minehip.unmarshal(payload).Lower == 0
+
+
+def test_server_writes_grow_for_escaped_data():
+    """An encoded Request can be ~6x its Data (control bytes become \\u00XX): writes() grows its
+    buffer to the reported size instead of failing on every later call."""
+    v = Server()
+    v.read(1, minehip.marshal(minehip.NewJoin()))
+    data = "\x01" * 5000                                     # 30,000 bytes once escaped
+    v.read(2, minehip.marshal(minehip.NewRequest(data, 0, 99)))
+    (c, payload), = v.writes()
+    m = minehip.unmarshal(payload)
+    assert c == 1 and m.Data == data.encode() and len(payload) > 6 * 5000
+    assert v.writes() == []

@@ -33,7 +33,8 @@ for s in $STEPS; do
       ;;
     tests)
       make -C "$ROOT" -q all 2>/dev/null || echo "WARNING: build outputs older than sources" | tee -a "$OUT/session.log"
-      timeout -k 10 900 python -m pytest "$ROOT/tests" -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+      timeout -k 10 900 python -u -m pytest "$ROOT/tests" -m gpu -v -x -p no:cacheprovider --timeout 150 \
+          --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/pytest_gpu.log"; fatal $rc
       ;;
     smoke)
@@ -41,12 +42,25 @@ for s in $STEPS; do
       rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       ;;
     bench)
-      timeout -k 10 600 python "$ROOT/bench.py" --steps 5 --warmup 1 > "$OUT/bench.json" 2> "$OUT/bench.err"
+      # the driver's command line (BENCH_rNN.json)
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; echo "bench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench.json"; fatal $rc
+      ;;
+    multi1)
+      # N = 1 through the in-process multi-device path (mh_search_multi, scheduler chunks)
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 1 --multi --steps 20 --warmup 5 --no-pmc --no-cpu-baseline \
+          > "$OUT/bench_multi1.json" 2> "$OUT/bench_multi1.err"
+      rc=$?; echo "multi1 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_multi1.json"; fatal $rc
+      ;;
+    cfg4)
+      # configs[3] (2^40, the scaling workload) on one GPU: 20 slices covering the whole range
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 1 --config 4 --steps 20 --warmup 1 --no-cpu-baseline \
+          > "$OUT/bench_cfg4.json" 2> "$OUT/bench_cfg4.err"
+      rc=$?; echo "cfg4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_cfg4.json"; fatal $rc
       ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+          -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
       ;;
@@ -106,19 +120,30 @@ for s in $STEPS; do
       timeout -k 10 300 python "$ROOT/tools/lsp_cluster_bench.py" --bits 38 --miners 2 --kill 2 > "$OUT/lsp_cluster_kill.json" 2> "$OUT/lsp_cluster_kill.err"
       rc=$?; echo "lspcluster kill rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/lsp_cluster_kill.json"; fatal $rc
       ;;
+    lspcfg4)
+      # BASELINE configs[4] at its stated size on one GPU: server + 3 GPU miner processes + client
+      # over LSP/UDP, 2^42 nonces, one miner SIGKILLed after 5 s; checked against a direct search
+      timeout -k 10 900 python "$ROOT/tools/lsp_cluster_bench.py" --bits 42 --miners 3 --kill 5 \
+          > "$OUT/lsp_cfg4.json" 2> "$OUT/lsp_cfg4.err"
+      rc=$?; echo "lspcfg4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/lsp_cfg4.json"; fatal $rc
+      ;;
     dist2)
-      # 2 ranks on the box's one GPU over gloo: exercises bench.py's multi-process path
+      # 2 ranks on the box's one GPU: bench.py's launched path (configs[3] layout, 2^36 to stay short)
       BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-          --master-addr 127.0.0.1 --master-port 29533 "$ROOT/bench.py" --gpus 2 --steps 2 --warmup 1 \
-          --dist-backend gloo > "$OUT/dist2.json" 2> "$OUT/dist2.err"
+          --master-addr 127.0.0.1 --master-port 29533 "$ROOT/bench.py" --gpus 2 --steps 4 --warmup 1 \
+          --bits 36 > "$OUT/dist2.json" 2> "$OUT/dist2.err"
       rc=$?; echo "dist2 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist2.json"; fatal $rc
       ;;
     dist8)
-      # 8 ranks on the box's one GPU over gloo: bench.py's N = 8 sharding and merge, golden-checked
+      # 8 ranks on the box's one GPU: bench.py's N = 8 sharding and host merge (2^36, golden-checked weak line too)
       BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
-          --master-addr 127.0.0.1 --master-port 29534 "$ROOT/bench.py" --gpus 8 --steps 1 --warmup 1 \
-          --dist-backend gloo > "$OUT/dist8.json" 2> "$OUT/dist8.err"
+          --master-addr 127.0.0.1 --master-port 29534 "$ROOT/bench.py" --gpus 8 --steps 4 --warmup 1 \
+          --bits 36 > "$OUT/dist8.json" 2> "$OUT/dist8.err"
       rc=$?; echo "dist8 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8.json"; fatal $rc
+      BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+          --master-addr 127.0.0.1 --master-port 29535 "$ROOT/bench.py" --gpus 8 --config 2 --bits 28 --steps 2 \
+          --warmup 1 > "$OUT/dist8_weak.json" 2> "$OUT/dist8_weak.err"
+      rc=$?; echo "dist8 weak rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8_weak.json"; fatal $rc
       ;;
     *) echo "unknown step $s";;
   esac

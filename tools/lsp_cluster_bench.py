@@ -21,6 +21,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,11 +40,21 @@ def main():
     ap.add_argument("--no-direct", action="store_true")
     a = ap.parse_args()
     hi = (1 << a.bits) - 1
+    t_start = time.perf_counter()
+    phase = ["start"]
+
+    def heartbeat():  # a long run prints something every 30 s (gpurun treats silence as a hang)
+        while True:
+            time.sleep(30)
+            print(f"[{time.perf_counter() - t_start:.0f} s] {phase[0]}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
 
     direct, t_direct = None, None
     if not a.no_direct:
         import minehip
         minehip.search(a.msg, 0, 10 ** 6)
+        phase[0] = f"direct mh_search of 2^{a.bits}"
         t0 = time.perf_counter()
         direct = minehip.search(a.msg, 0, hi)
         t_direct = time.perf_counter() - t0
@@ -71,6 +82,7 @@ def main():
         cl = subprocess.Popen([os.path.join(BIN, "minehip-client"), hp, a.msg, str(hi)], stdout=subprocess.PIPE,
                               env=env, text=True)
         procs.append(cl)
+        phase[0] = f"LSP cluster, {a.miners} miner(s)"
         if a.kill is not None:
             time.sleep(a.kill)
             miners[-1].kill()

@@ -1,10 +1,11 @@
 """pmc_launch.py -- the process `bench.py` runs under `rocprofv3 --pmc` to
-measure the HBM traffic of its dominant kernel (roofline.traffic).
+measure the counters of its largest kernels (roofline.traffic, roofline.pmc).
 
-One search of exactly the nonces the dominant fast_search launch covers in
-the bench's own plan, so the counters of that dispatch are per launch:
+One search per given range, each exactly the nonces one fast_search launch
+covers in the bench's own plan, so the counters of those dispatches are per
+launch:
 
-  python tools/pmc_launch.py <msg> <lower> <upper> [dev]
+  python tools/pmc_launch.py <msg> <dev> <lower>:<upper> [<lower>:<upper> ...]
 
 No torch: only libminehip (ctypes), so the profiled process starts in ~1 s.
 """
@@ -18,9 +19,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
 def main():
     import minehip
     msg = sys.argv[1].encode()
-    lo, hi = int(sys.argv[2]), int(sys.argv[3])
-    dev = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-    print(minehip.search(msg, lo, hi, dev), flush=True)
+    dev = int(sys.argv[2])
+    for r in sys.argv[3:]:
+        lo, hi = (int(x) for x in r.split(":"))
+        print(minehip.search(msg, lo, hi, dev), flush=True)
 
 
 if __name__ == "__main__":
