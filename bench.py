@@ -412,6 +412,9 @@ def main():
     ap.add_argument("--msg", default=None, help="override the config's message")
     ap.add_argument("--bits", type=int, default=None, help="override log2 nonces per GPU (weak) / total (strong)")
     ap.add_argument("--multi", action="store_true", help="N = 1 through mh_search_multi (the in-process path)")
+    ap.add_argument("--devices", default=None,
+                    help="in-process path: comma-separated device list (default 0..N-1); repeats rehearse "
+                         "N workers on fewer GPUs, e.g. --gpus 4 --devices 0,0,0,0 on a 1-GPU box")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     args = ap.parse_args()
@@ -443,6 +446,10 @@ def main():
         if local >= ndev:
             die(f"rank {rank}: HIP device {local} not visible ({ndev} visible)")
         devs = [local]
+    elif args.devices:
+        devs = [int(x) for x in args.devices.split(",")]
+        if len(devs) != args.gpus or any(d < 0 or d >= ndev for d in devs):
+            die(f"--devices {args.devices}: need {args.gpus} entries in [0, {ndev})")
     else:
         if ndev < args.gpus:
             die(f"--gpus {args.gpus} but {ndev} HIP device(s) visible")
@@ -461,6 +468,7 @@ def main():
     steps = args.steps
     multi = (not launched) and (n_gpus > 1 or args.multi)
     done = {d: 0 for d in devs}  # nonces searched per device in the timed region
+    uniq = sorted(set(devs))
 
     def step(k, timed=False):
         if launched:
@@ -477,11 +485,11 @@ def main():
     barrier = (lambda: dist.barrier()) if launched else (lambda: None)
     for w in range(args.warmup):
         step(w)
-    for d in devs:
+    for d in uniq:
         minehip.profile_enable(d, True)
     r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize)
     per_dev = []
-    for d in devs:
+    for d in uniq:
         pr = minehip.profile_read(d)
         per_dev.append({"dev": d, "rank": rank, "prof": pr, "kstats": minehip.profile_kernels(d)})
         minehip.profile_enable(d, False)

@@ -36,7 +36,7 @@ int run_stdio(const std::vector<int>& devs) {
     while (std::getline(std::cin, line)) {
         size_t n = 0;
         const int rc = mh_miner_handle(devs.data(), (int)devs.size(), line.data(), line.size(), out, sizeof out, &n);
-        if (rc == MH_EINVAL || rc == MH_ERANGE) continue;  // not a (valid) Request: ignored
+        if (rc == MH_ENOTREQ || rc == MH_ERANGE) continue;  // not a (valid) Request: ignored
         if (rc != MH_OK) {
             fprintf(stderr, "minehip: %s\n", mh_last_error());
             return 1;

@@ -51,6 +51,13 @@ for s in $STEPS; do
       timeout -k 10 600 python "$ROOT/bench.py" --gpus 1 --multi --steps 20 --warmup 5 --no-pmc --no-cpu-baseline \
           > "$OUT/bench_multi1.json" 2> "$OUT/bench_multi1.err"
       rc=$?; echo "multi1 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_multi1.json"; fatal $rc
+      # the scheduler path itself: 4 worker threads on the one GPU, configs[3] slices (2^38 to stay short)
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 4 --devices 0,0,0,0 --bits 38 --steps 8 --warmup 1 \
+          > "$OUT/bench_multi4.json" 2> "$OUT/bench_multi4.err"
+      rc=$?; echo "multi4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_multi4.json"; fatal $rc
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 1 --config 4 --bits 38 --steps 8 --warmup 1 --no-pmc \
+          --no-cpu-baseline > "$OUT/bench_single38.json" 2> "$OUT/bench_single38.err"
+      rc=$?; echo "single38 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/bench_single38.json"; fatal $rc
       ;;
     cfg4)
       # configs[3] (2^40, the scaling workload) on one GPU: 20 slices covering the whole range
