@@ -44,7 +44,15 @@ asm: $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
 # VALU issue-rate microbenchmarks, run by tools/gpu_session.sh
-probes: build/valu_peak build/valu_ops build/valu_mix
+probes: build/valu_peak build/valu_ops build/valu_mix build/valu_pair build/valu_bank
+build/valu_bank: tools/gen_valu_bank.py
+	mkdir -p build
+	python3 tools/gen_valu_bank.py
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ tools/valu_bank.hip
+build/valu_pair: tools/gen_valu_pair.py
+	mkdir -p build
+	python3 tools/gen_valu_pair.py
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ tools/valu_pair.hip
 build/valu_mix: tools/gen_valu_mix.py
 	mkdir -p build
 	python3 tools/gen_valu_mix.py

@@ -21,7 +21,12 @@
 // Every candidate comparison is the lexicographic (hash, nonce) order, which
 // equals the reference loop's strict-< first minimum.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "layout.hpp"
 #include "sha256_gfx950.hpp"
@@ -346,6 +351,9 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
+#if defined(MH_SYNC) && MH_SYNC == 10
+        __builtin_amdgcn_s_barrier();
+#endif
         // digits 0..L-2 of q = 10*g + i: wave-uniform, so this is SALU work
         uint32_t cj = 0u, cjm = 0u, gq = g;
         for (uint32_t k = a.L - 1u; k-- > 0u;) {
@@ -382,6 +390,9 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 
         for (uint32_t i = 0; i < 10u; ++i) {
             // ---- per nonce ------------------------------------------------
+#if defined(MH_SYNC) && MH_SYNC == 1
+            __builtin_amdgcn_s_barrier();
+#endif
             const uint32_t inc = i << sh_last;  // SALU
             const uint32_t s0inc = kIncSigma.s0[sh_last >> 3][i], s1inc = kIncSigma.s1[sh_last >> 3][i];
             uint32_t x[64];
@@ -532,7 +543,39 @@ static hipError_t launch_fast_t(const FastArgs& a, Partial* partials, uint32_t b
     case j:           \
         return launch_fast_t<j, m>(a, partials, blocks, s);
 
+// MINEHIP_DEV_CODE_OBJECT (experiments only, tools/isa_variant.py): launch
+// fast_search<J, MODE> from this gfx950 code object instead of the built-in
+// one -- the same kernel with hand-edited ISA, A/B'd in one process.  Read
+// on every launch so tools/kbench.py can interleave variants.
+static hipError_t launch_fast_dev(const char* path, int J, int mode, const FastArgs& a, Partial* partials,
+                                  uint32_t blocks, hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::string, hipModule_t> mods;
+    hipModule_t mod;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = mods.find(path);
+        if (it == mods.end()) {
+            hipError_t e = hipModuleLoad(&mod, path);
+            if (e != hipSuccess) return e;
+            it = mods.emplace(path, mod).first;
+        }
+        mod = it->second;
+    }
+    char name[96];
+    snprintf(name, sizeof name, "_ZN2mh11fast_searchILi%dELi%dEEEvNS_8FastArgsEPNS_7PartialE", J, mode);
+    hipFunction_t f;
+    hipError_t e = hipModuleGetFunction(&f, mod, name);
+    if (e != hipSuccess) return e;
+    FastArgs args = a;
+    Partial* out = partials;
+    void* params[] = {&args, &out};
+    return hipModuleLaunchKernel(f, blocks, 1, 1, kBlockThreads, 1, 1, 0, s, params, nullptr);
+}
+
 hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {
+    if (const char* co = getenv("MINEHIP_DEV_CODE_OBJECT"); co && *co)
+        return launch_fast_dev(co, J, mode, a, partials, blocks, s);
     if (mode == kModeOne) {
         switch (J) {
             MH_CASE(0, kModeOne) MH_CASE(1, kModeOne) MH_CASE(2, kModeOne) MH_CASE(3, kModeOne)

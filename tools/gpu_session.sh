@@ -101,6 +101,14 @@ for s in $STEPS; do
       timeout -k 10 300 "$ROOT/build/valu_mix" > "$OUT/valu_mix.json" 2>&1
       rc=$?; echo "valumix rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_mix.json"; fatal $rc
       ;;
+    valupair)
+      timeout -k 10 300 "$ROOT/build/valu_pair" > "$OUT/valu_pair.json" 2>&1
+      rc=$?; echo "valupair rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_pair.json"; fatal $rc
+      ;;
+    valubank)
+      timeout -k 10 300 "$ROOT/build/valu_bank" > "$OUT/valu_bank.json" 2>&1
+      rc=$?; echo "valubank rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/valu_bank.json"; fatal $rc
+      ;;
     kbench)
       timeout -k 10 600 python "$ROOT/tools/kbench.py" ${KBENCH_ARGS:-} > "$OUT/kbench.json" 2> "$OUT/kbench.err"
       rc=$?; echo "kbench rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/kbench.json"; tail -3 "$OUT/kbench.err"; fatal $rc

@@ -1,0 +1,116 @@
+"""Build gfx950 code objects of search_kernels.hip with hand-edited ISA, for
+A/B runs through the library's MINEHIP_DEV_CODE_OBJECT hook (experiments
+only).
+
+  python tools/isa_variant.py base e64      # -> build/isa/<variant>.hsaco
+  python tools/kbench.py --var base:MINEHIP_DEV_CODE_OBJECT=build/isa/base.hsaco \
+                         --var e64:MINEHIP_DEV_CODE_OBJECT=build/isa/e64.hsaco
+
+Variants (edits apply inside the fast_search kernels only):
+  base  the compiler's assembly, re-assembled unchanged (control for the hook)
+  e64   every VOP2 v_add_u32 / v_lshrrev_b32 without a literal operand in its
+        VOP3 (_e64) encoding: same operation, other encoding.  The r02e probes
+        (tools/gen_valu_pair.py) show a VOP3 full-rate op after a half-rate
+        one co-issuing where a VOP2 one does not (HF3 3.74 vs HF 4.03 cycles).
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "bitcoin-miner_amd", "csrc")
+OUT = os.path.join(ROOT, "build", "isa")
+HIPCC = "/opt/rocm/bin/hipcc"
+LLVM = "/opt/rocm/lib/llvm/bin"
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950"]
+
+
+def compile_s(path, extra=()):
+    subprocess.run([HIPCC, *FLAGS, *extra, "--cuda-device-only", "-S", "-o", path,
+                    os.path.join(CSRC, "search_kernels.hip")], check=True)
+
+
+def assemble(s_path, co_path):
+    o_path = co_path[:-6] + ".o"
+    subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                    s_path, "-o", o_path], check=True)
+    subprocess.run([f"{LLVM}/ld.lld", "-shared", o_path, "-o", co_path], check=True)
+
+
+INLINE = re.compile(r"^-?\d+$")
+
+
+def is_inline(op):
+    op = op.strip()
+    if op.startswith(("v", "s", "vcc", "exec", "m0")) and not op.startswith("0x"):
+        return True
+    if INLINE.match(op):
+        return -16 <= int(op) <= 64
+    return False
+
+
+def to_e64(line, ops=("v_add_u32", "v_lshrrev_b32")):
+    m = re.match(r"^(\s+)(" + "|".join(ops) + r")_e32\s+(.*)$", line)
+    if not m:
+        return line, False
+    args = [a.strip() for a in m.group(3).split(",")]
+    if not all(is_inline(a) for a in args[1:]):
+        return line, False  # gfx9 VOP3 takes no literal
+    return f"{m.group(1)}{m.group(2)}_e64 {', '.join(args)}", True
+
+
+def in_fast(text):
+    """Yield (line, inside a fast_search function body)."""
+    inside = False
+    for line in text.split("\n"):
+        if re.match(r"^_ZN2mh11fast_search\S*:", line):
+            inside = True
+        elif inside and (line.startswith(".Lfunc_end") or "s_endpgm" in line):
+            yield line, True
+            inside = False
+            continue
+        yield line, inside
+
+
+# source-level variants: the kernel source compiled with extra defines
+DEFINES = {
+    "sync1": ["-DMH_SYNC=1"],    # s_barrier before every nonce: the 4 waves of a workgroup in step
+    "sync10": ["-DMH_SYNC=10"],  # s_barrier before every group of 10 nonces
+}
+
+
+def variant(name, base_text):
+    if name == "base":
+        return base_text, 0
+    if name == "e64":
+        out, n = [], 0
+        for line, fast in in_fast(base_text):
+            if fast:
+                line, ch = to_e64(line)
+                n += ch
+            out.append(line)
+        return "\n".join(out), n
+    raise SystemExit(f"unknown variant {name}")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    base_s = os.path.join(OUT, "base.s")
+    compile_s(base_s)
+    text = open(base_s).read()
+    for name in sys.argv[1:] or ["base", "e64"]:
+        s_path = os.path.join(OUT, f"{name}.s")
+        if name in DEFINES:
+            compile_s(s_path, DEFINES[name])
+            n = 0
+        else:
+            t, n = variant(name, text)
+            if name != "base":
+                open(s_path, "w").write(t)
+        assemble(s_path, os.path.join(OUT, f"{name}.hsaco"))
+        print(f"{name}: {n} instructions edited -> build/isa/{name}.hsaco")
+
+
+if __name__ == "__main__":
+    main()
