@@ -314,8 +314,9 @@ def pmc_derived(v, piece, cus):
         "valu_active_of_wave_cycles": round(v["SQ_ACTIVE_INST_VALU"] / wc, 4),
         "wait_inst_any_of_wave_cycles": round(v["SQ_WAIT_INST_ANY"] / wc, 4),
         "wait_any_of_wave_cycles": round(v["SQ_WAIT_ANY"] / wc, 4),
-        # VALU busy per SIMD (rocprof's VALUBusy: ACTIVE_INST_VALU x 4 quad->cycles / SIMD-cycles)
-        "valu_busy": round(v["SQ_ACTIVE_INST_VALU"] * 4 / (cycles * simds), 4),
+        # VALU instructions issued per SIMD quad-cycle (SQ_ACTIVE_INST_VALU counts one per instruction,
+        # calibrated on tools/gen_valu_pair.py probes): 1 = one per quad, 2 = a pair in every quad
+        "valu_instr_per_quad": round(v["SQ_ACTIVE_INST_VALU"] * 4 / (cycles * simds), 4),
         # quad-cycles in which a SIMD issued two VALU instructions, per SIMD quad-cycle
         "valu2_of_simd_quads": round(v["SQ_ACTIVE_INST_VALU2"] / (cycles * simds / 4), 4),
         "counters": {k: v[k] for k in sorted(v) if not k.startswith("dur_ns")},
