@@ -37,6 +37,30 @@ PATTERNS = {
     # dependent pairs: H then B reading H's result (the Sigma shape)
     "HB_DEP": [H, B], "HBB_DEP": [H, B, B], "HF3_DEP": [H, F3],
 }
+# r02o: priority phases.  s_setprio is a scalar instruction (no VALU slot).  A wave entering a run
+# of full-rate ops raises its priority, so the arbiter prefers waves whose next VALU op can pair
+P3, P0 = "s_setprio 3", "s_setprio 0"
+PATTERNS.update({
+    "H4F4": [H] * 4 + [F] * 4, "H4F4_PRIO": [P0] + [H] * 4 + [P3] + [F] * 4,
+    "H6F4": [H] * 6 + [F] * 4, "H6F4_PRIO": [P0] + [H] * 6 + [P3] + [F] * 4,
+    "H4B4": [H] * 4 + [B] * 4, "H4B4_PRIO": [P0] + [H] * 4 + [P3] + [B] * 4,
+    "H8F8": [H] * 8 + [F] * 8, "H8F8_PRIO": [P0] + [H] * 8 + [P3] + [F] * 8,
+    "H4F4_PRIOINV": [P3] + [H] * 4 + [P0] + [F] * 4,
+    "H2F2_PRIO": [P0] + [H] * 2 + [P3] + [F] * 2,
+    "H9F5_PRIO": [P0] + [H] * 9 + [P3] + [B] * 4 + [F],
+    # r02p: priority on the HALF-rate phase (the wave about to issue full-rate ops yields)
+    "H4B4_PRIOINV": [P3] + [H] * 4 + [P0] + [B] * 4,
+    "H6F4_PRIOINV": [P3] + [H] * 6 + [P0] + [F] * 4,
+    "H2F2_PRIOINV": [P3] + [H] * 2 + [P0] + [F] * 2,
+    "HF_PRIOINV": [P3, H, P0, F],
+    "HB_PRIOINV": [P3, H, P0, B],
+    "H9F5_PRIOINV": [P3] + [H] * 9 + [P0] + [B] * 4 + [F],
+    "H4F4_PRIOINV1": ["s_setprio 1"] + [H] * 4 + [P0] + [F] * 4,
+    "H4A3F4_PRIOINV": [P3] + [H, A3, H, A3] + [P0] + [F] * 4,
+    "ROUND_PRIOINV": [P3, H, H, H, P0, B, B, P3, H, H, H, A3, P0, B, B, P3, A3, A3, P0, F],
+    "ROUND_GRP_PRIOINV": [P3, H, H, H, H, H, H, A3, A3, A3, P0, B, B, B, B, F],
+    "F4H4_PRIOINV": [P0] + [F] * 4 + [P3] + [H] * 4,
+})
 DEP = {"HB_DEP", "HBB_DEP", "HF3_DEP"}
 # r02h: loop-body size (instruction-fetch footprint): the same stream unrolled to ~1K / 2.5K / 5K
 # instructions per loop iteration (the per-nonce loop is 1,196 instructions, ~8.8 KB)
@@ -55,6 +79,9 @@ def lines_of(name, seq):
     idx = 0
     for r in range(reps):
         for k, ins in enumerate(seq):
+            if ins.startswith("s_"):
+                out.append(ins)
+                continue
             c = (idx // len(seq)) % 8 if name in DEP else idx % 8
             idx += 1
             out.append(ins.format(x="%" + str(c), y="%8"))
@@ -66,7 +93,7 @@ kernels = []
 for name, seq in PATTERNS.items():
     lines = lines_of(name, seq)
     asm = "\\n\\t".join(lines)
-    kernels.append((name, len(lines)))
+    kernels.append((name, sum(1 for l in lines if not l.startswith("s_"))))
     body.append(f'''
 __global__ __launch_bounds__(256) void k_{name}(uint32_t* out, uint32_t s, uint64_t* clk) {{
     uint32_t x0 = threadIdx.x ^ s, x1 = x0 * 3, x2 = x0 * 5, x3 = x0 * 7, x4 = x0 * 9, x5 = x0 * 11,

@@ -91,7 +91,45 @@ def variant(name, base_text):
                 n += ch
             out.append(line)
         return "\n".join(out), n
+    if name.startswith("prio"):
+        return prio_phases(base_text)
     raise SystemExit(f"unknown variant {name}")
+
+
+# half-rate VALU ops on gfx950 (tools/isa_report.py, measured by tools/valu_ops.hip)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from isa_report import HALF_RATE  # noqa: E402
+
+
+def valu_class(line):
+    m = re.match(r"^\s+(v_\w+)", line)
+    if not m:
+        return None
+    op = m.group(1)
+    if op in HALF_RATE or op.rsplit("_e32", 1)[0] in HALF_RATE or op.rsplit("_e64", 1)[0] in HALF_RATE:
+        return "H"
+    return "F"
+
+
+def prio_phases(text):
+    """s_setprio 3 before every run of half-rate VALU ops, s_setprio 0 before every run of
+    full-rate ones (r02p probes: ROUND 4.07 -> 3.20 cycles per instruction): a wave about to
+    issue full-rate ops yields the arbiter to waves in a half-rate run, and its full-rate op
+    then co-issues beside their half-rate one."""
+    out, n = [], 0
+    for line, fast in in_fast(text):
+        if fast:
+            if re.match(r"^\.LBB|^_ZN", line):
+                cur = None
+            c = valu_class(line)
+            if c is not None and c != cur:
+                out.append(f"\ts_setprio {3 if c == 'H' else 0}")
+                n += 1
+                cur = c
+        else:
+            cur = None
+        out.append(line)
+    return "\n".join(out), n
 
 
 def main():
