@@ -8,7 +8,15 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSRC)/message.cpp \
            $(CSRC)/sched.cpp $(CSRC)/server.cpp
 HDRS    := $(CSRC)/layout.hpp $(CSRC)/plan.hpp $(CSRC)/sha256_gfx950.hpp $(CSRC)/msgcodec.hpp \
-           $(CSRC)/sched.hpp include/minehip.h include/minehip_server.h
+           $(CSRC)/sched.hpp $(CSRC)/kernel_common.hpp include/minehip.h include/minehip_server.h
+LLVM    ?= /opt/rocm/lib/llvm/bin
+BUILD   := build
+FAST_HDRS := $(CSRC)/kernel_common.hpp $(CSRC)/layout.hpp $(CSRC)/sha256_gfx950.hpp
+FAST_S  := $(BUILD)/fast_search.s
+FAST_PS := $(BUILD)/fast_search_prio.s
+FAST_CO := $(BUILD)/fast_search.hsaco
+FAST_O  := $(BUILD)/fast_co.o
+FASTFLAGS ?=
 
 LSPLIB  := $(PKG)/minehip/liblsp440.so
 APPS    := $(CSRC)/apps
@@ -22,8 +30,21 @@ all: $(LIB) $(LSPLIB) $(CLIS) oracle
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
 	g++ -O2 -std=c++17 -Wall -Wextra -fPIC -shared -o $@ $(CSRC)/lsp/lsp.cpp -lpthread
 
-$(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+$(LIB): $(SRCS) $(HDRS) $(FAST_O)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -x none $(FAST_O)
+
+# fast_search<J, MODE>: gfx950 assembly -> issue-priority pass (s_setprio around half-/full-rate
+# runs) -> code object -> embedded in the library (fast_co.S)
+$(FAST_S): $(CSRC)/fast_search.hip $(FAST_HDRS)
+	mkdir -p $(BUILD)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $(FASTFLAGS) --cuda-device-only -S -o $@ $<
+$(FAST_PS): $(FAST_S) $(CSRC)/issue_prio.py
+	python3 $(CSRC)/issue_prio.py $< $@
+$(FAST_CO): $(FAST_PS)
+	$(LLVM)/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c -o $(BUILD)/fast_search_prio.o $<
+	$(LLVM)/ld.lld -shared -o $@ $(BUILD)/fast_search_prio.o
+$(FAST_O): $(CSRC)/fast_co.S $(FAST_CO)
+	gcc -c -fPIC -Wa,-I,$(BUILD) -o $@ $<
 
 # native C++ callers of the C-ABI (rpath: the library next to the package)
 $(BIN)/minehip-search: $(CSRC)/cli.cpp include/minehip.h $(LIB)
@@ -39,7 +60,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 # disassembly + register report of the kernels (for DESIGN.md / profiling)
-asm: $(SRCS) $(HDRS)
+asm: $(FAST_PS)
 	mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/search_kernels.s $(CSRC)/search_kernels.hip
 
@@ -62,7 +83,7 @@ build/valu_%: tools/valu_%.hip
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 clean:
-	rm -f $(LIB) $(LSPLIB) $(CLIS)
+	rm -f $(LIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_PS) $(FAST_CO) $(FAST_O) $(BUILD)/fast_search_prio.o
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean probes

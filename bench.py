@@ -33,8 +33,8 @@ Rank 0 prints ONE JSON line.  `roofline` is priced on SURVEY §8(d) D4's
 algorithmic basis (1,616 int32 VALU ops per SHA-256 compression x tail blocks
 per nonce) over the dominant kernel's HIP-event launch time, against the VALU
 peak 256 CU x 128 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: 4 SIMD-32 per CU);
-`roofline.slot_util` is the same kernel in the issue slots its compiled loop
-occupies.  At N = 1, rocprofv3 --pmc passes over one launch of
+`roofline.issue` is the same kernel's instruction issue against 2 VALU instructions
+per SIMD quad-cycle.  At N = 1, rocprofv3 --pmc passes over one launch of
 each of the two largest kernels give HBM traffic and the SQ counters
 (`roofline.pmc`).  `cpu_baseline` times the CPU port of the reference loop
 (oracle/) on a bounded sample, at N = 1 only.
@@ -305,7 +305,7 @@ def pmc_derived(v, piece, cus):
         "pmc_launch_ms": round(dur / 1e6, 3),
         "nonces": nonces,
         "valu_instr_per_nonce": round(v["SQ_INSTS_VALU"] * 64 / nonces, 1),
-        # SIMD cycles per issued wave64 VALU instruction (2 = every issue slot used)
+        # SIMD cycles per issued wave64 VALU instruction (2 = two per quad-cycle, the issue peak)
         "cycles_per_valu_instr": round(cycles * simds / v["SQ_INSTS_VALU"], 3),
         # mean resident waves per SIMD over the launch (occupancy)
         "waves_per_simd": round(wc * 4 / (cycles * simds), 2),
@@ -357,7 +357,7 @@ def kernel_totals(per_dev_kstats):
 def roofline(kst, cus, n_devices):
     """Roofline of the dominant kernel from its HIP-event launch times (summed
     over devices, so achieved is per GPU).  frac is on SURVEY §8(d) D4's
-    algorithmic basis; slot_util counts the issue slots of the compiled loop."""
+    algorithmic basis; issue counts the instructions its compiled loop issues."""
     peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
     if not kst:
         return {"bound": "valu", "achieved": None, "peak": round(peak, 3), "frac": None}
@@ -367,7 +367,9 @@ def roofline(kst, cus, n_devices):
     ghs = dom["nonces"] / sec / 1e9
     alg = dom["nonces"] * SURVEY_OPS_PER_COMPRESSION * blocks  # int32 ops, §8(d) D4
     achieved = alg / sec / 1e12
-    slots = dom["slots"] / sec / 1e12           # lane issue slots (one nonce = one lane)
+    ops = dom["ops"]                             # lane-instructions of the per-nonce loops
+    n_instr = dom["ops"] / max(1, dom["nonces"])
+    n_half = (dom["slots"] - dom["ops"]) / max(1, dom["nonces"])  # slots count a half-rate op twice
     launches = max(1, dom["launches"])
     line = {
         "bound": "valu",
@@ -379,6 +381,9 @@ def roofline(kst, cus, n_devices):
         "basis": f"SURVEY §8(d) D4: {SURVEY_OPS_PER_COMPRESSION} ops per compression x {blocks} tail block(s) "
                  f"per nonce over the dominant kernel's HIP-event launch time; peak {cus} CU x "
                  f"{LANES_PER_CU_CLK} lanes/clk x {PEAK_SCLK_HZ / 1e9} GHz",
+        "frac_note": "D4 prices a nonce at full compressions; the loop hoists the work shared by a "
+                     "lane's nonces and issues fewer instructions, so this fraction credits the hoisting "
+                     "and can exceed 1.  The hardware fraction is issue.frac.",
         "kernel": dom["name"],
         "tail_blocks": blocks,
         "launches": dom["launches"],
@@ -387,12 +392,18 @@ def roofline(kst, cus, n_devices):
         "nonces_per_launch": dom["nonces"] // launches,
         "alg_ops_per_launch": alg // launches,
         "kernel_ghs": round(ghs, 4),
-        "slot_util": {
-            "achieved": round(slots, 3), "peak": round(peak, 3), "frac": round(slots / peak, 4),
-            "slots_per_nonce": round(dom["slots"] / max(1, dom["nonces"]), 1),
-            "instr_per_nonce": round(dom["ops"] / max(1, dom["nonces"]), 1),
-            "note": "issue slots of the compiled per-nonce loop (full-rate op 1, half-rate v_alignbit/"
-                    "v_add3 2; DESIGN.md §4), hoisted run/group work excluded"},
+        # VALU issue: one instruction per SIMD quad-cycle, two when the second is full rate (a
+        # full-rate op beside a half-rate or full-rate one) -> peak 2 per quad =
+        # 128 lane-instructions/clk/CU, the same 78.64 T.  A nonce is one lane, so lane-instructions/s
+        # = nonces/s x instructions per nonce.  The mix bound: a half-rate op cannot share its
+        # quad-cycle with another half-rate op, so a nonce needs >= max(H, N/2) quad-cycles.
+        "issue": {
+            "achieved": round(ops / sec / 1e12, 3), "peak": round(peak, 3), "frac": round(ops / sec / 1e12 / peak, 4),
+            "instr_per_nonce": round(n_instr, 1), "half_rate_per_nonce": round(n_half, 1),
+            "mix_bound_frac": round(n_instr / (2 * max(n_half, n_instr / 2)), 4),
+            "note": "lane-instructions/s of the compiled per-nonce loop (hoisted run/group work excluded) "
+                    "against 2 VALU instructions per SIMD quad-cycle; mix_bound_frac = the most this "
+                    "loop's half-/full-rate mix can reach"},
         "full_compression_instr": OPS_PER_BLOCK,
     }
     if len(kst) > 1:
@@ -548,8 +559,8 @@ def main():
             # achieved / frac again at the clock this launch ran at
             at = roof["pmc"]["sclk_ghz"] * 1e9
             roof["pmc"]["frac_alg_at_sclk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
-            roof["pmc"]["slot_util_at_sclk"] = round(roof["slot_util"]["achieved"]
-                                                     / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+            roof["pmc"]["issue_frac_at_sclk"] = round(roof["issue"]["achieved"]
+                                                      / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
             if len(pieces) > 1:
                 v1 = vals[f"fast_search<{pieces[1]['word']}, {pieces[1]['mode']}>"]
                 roof["second_kernel"]["pmc"] = pmc_derived(v1, pieces[1], cus)

@@ -26,7 +26,9 @@
 #include "sched.hpp"
 
 namespace mh {
-hipError_t launch_fast(int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
+hipError_t fast_module_init(int dev);
+hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks,
+                       hipStream_t s);
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
                              hipStream_t s);
@@ -136,6 +138,7 @@ int init_locked(DevCtx* c, int dev) {
         MH_HIP(hipEventCreate(&t.start));
         MH_HIP(hipEventCreate(&t.stop));
     }
+    MH_HIP(mh::fast_module_init(dev));  // the fast_search code object (issue-priority build)
     c->dev = dev;
     c->ready = true;
     return MH_OK;
@@ -196,7 +199,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
         MH_HIP(hipEventRecord(tm->start, c->stream));
     }
     if (p.kind == 0)
-        MH_HIP(mh::launch_fast(p.J, p.mode, p.fa, out, blocks, c->stream));
+        MH_HIP(mh::launch_fast(c->dev, p.J, p.mode, p.fa, out, blocks, c->stream));
     else
         MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, c->stream));
     if (tm) MH_HIP(hipEventRecord(tm->stop, c->stream));

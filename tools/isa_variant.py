@@ -2,12 +2,14 @@
 A/B runs through the library's MINEHIP_DEV_CODE_OBJECT hook (experiments
 only).
 
-  python tools/isa_variant.py base e64      # -> build/isa/<variant>.hsaco
+  python tools/isa_variant.py base e64      # -> build/isa/<variant>.hsaco (from fast_search.hip)
   python tools/kbench.py --var base:MINEHIP_DEV_CODE_OBJECT=build/isa/base.hsaco \
                          --var e64:MINEHIP_DEV_CODE_OBJECT=build/isa/e64.hsaco
 
 Variants (edits apply inside the fast_search kernels only):
-  base  the compiler's assembly, re-assembled unchanged (control for the hook)
+  base  the compiler's assembly, re-assembled unchanged: the kernels WITHOUT the
+        issue-priority pass the library's own build applies
+  prio  the library's build (bitcoin-miner_amd/csrc/issue_prio.py), re-made here
   e64   every VOP2 v_add_u32 / v_lshrrev_b32 without a literal operand in its
         VOP3 (_e64) encoding: same operation, other encoding.  The r02e probes
         (tools/gen_valu_pair.py) show a VOP3 full-rate op after a half-rate
@@ -28,7 +30,7 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950"]
 
 def compile_s(path, extra=()):
     subprocess.run([HIPCC, *FLAGS, *extra, "--cuda-device-only", "-S", "-o", path,
-                    os.path.join(CSRC, "search_kernels.hip")], check=True)
+                    os.path.join(CSRC, "fast_search.hip")], check=True)
 
 
 def assemble(s_path, co_path):
@@ -96,40 +98,12 @@ def variant(name, base_text):
     raise SystemExit(f"unknown variant {name}")
 
 
-# half-rate VALU ops on gfx950 (tools/isa_report.py, measured by tools/valu_ops.hip)
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from isa_report import HALF_RATE  # noqa: E402
-
-
-def valu_class(line):
-    m = re.match(r"^\s+(v_\w+)", line)
-    if not m:
-        return None
-    op = m.group(1)
-    if op in HALF_RATE or op.rsplit("_e32", 1)[0] in HALF_RATE or op.rsplit("_e64", 1)[0] in HALF_RATE:
-        return "H"
-    return "F"
+sys.path.insert(0, CSRC)
+from issue_prio import annotate  # noqa: E402
 
 
 def prio_phases(text):
-    """s_setprio 3 before every run of half-rate VALU ops, s_setprio 0 before every run of
-    full-rate ones (r02p probes: ROUND 4.07 -> 3.20 cycles per instruction): a wave about to
-    issue full-rate ops yields the arbiter to waves in a half-rate run, and its full-rate op
-    then co-issues beside their half-rate one."""
-    out, n = [], 0
-    for line, fast in in_fast(text):
-        if fast:
-            if re.match(r"^\.LBB|^_ZN", line):
-                cur = None
-            c = valu_class(line)
-            if c is not None and c != cur:
-                out.append(f"\ts_setprio {3 if c == 'H' else 0}")
-                n += 1
-                cur = c
-        else:
-            cur = None
-        out.append(line)
-    return "\n".join(out), n
+    return annotate(text)
 
 
 def main():
