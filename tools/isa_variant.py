@@ -76,9 +76,13 @@ def in_fast(text):
 
 
 # source-level variants: the kernel source compiled with extra defines
-DEFINES = {
-    "sync1": ["-DMH_SYNC=1"],    # s_barrier before every nonce: the 4 waves of a workgroup in step
-    "sync10": ["-DMH_SYNC=10"],  # s_barrier before every group of 10 nonces
+DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
+    "sync1": (["-DMH_SYNC=1"], False),    # s_barrier before every nonce: the 4 waves of a workgroup in step
+    "sync10": (["-DMH_SYNC=10"], False),  # s_barrier before every group of 10 nonces
+    "prio_w8": (["-DMH_MIN_WAVES=8"], True),   # <= 64 VGPRs: 8 waves/SIMD
+    "prio_w6": (["-DMH_MIN_WAVES=6"], True),
+    "prio_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], True),
+    "prio_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], True),
 }
 
 
@@ -93,6 +97,15 @@ def variant(name, base_text):
                 n += ch
             out.append(line)
         return "\n".join(out), n
+    if name.startswith("a3split"):
+        # a3split<k>: every k-th v_add3_u32 of the fast kernels as two full-rate adds, then the
+        # issue-priority pass.  A half-rate op cannot share its quad-cycle with another half-rate
+        # op, so the loop needs >= max(H, N/2) quad-cycles; trading some add3 (1 H) for two adds
+        # (2 F) lowers H below N/2's growth (J = 4: H 701, N 1196).
+        k = int(name[len("a3split"):])
+        t, n = split_add3(base_text, k)
+        t2, n2 = prio_phases(t)
+        return t2, n + n2
     if name.startswith("prio"):
         return prio_phases(base_text)
     raise SystemExit(f"unknown variant {name}")
@@ -100,6 +113,38 @@ def variant(name, base_text):
 
 sys.path.insert(0, CSRC)
 from issue_prio import annotate  # noqa: E402
+
+
+def is_vgpr(op):
+    return re.match(r"^v\d+$", op) is not None
+
+
+def split_add3(text, k):
+    out, n, i = [], 0, 0
+    for line, fast in in_fast(text):
+        m = re.match(r"^(\s+)v_add3_u32\s+(\S+),\s*(\S+),\s*(\S+),\s*(\S+)\s*$", line) if fast else None
+        if m:
+            i += 1
+            if i % k == 0:
+                ind, d, a, b, c = m.groups()
+                ops = [a, b, c]
+                # the operand added second must not be the destination (the first add overwrites it)
+                last = next((x for x in reversed(ops) if x != d), None)
+                if last is not None:
+                    ops.remove(last)
+                    x, y = ops
+                    if is_vgpr(y):
+                        first = f"{ind}v_add_u32_e32 {d}, {x}, {y}"
+                    elif is_vgpr(x):
+                        first = f"{ind}v_add_u32_e32 {d}, {y}, {x}"
+                    else:
+                        first = f"{ind}v_add_u32_e64 {d}, {x}, {y}"
+                    out.append(first)
+                    out.append(f"{ind}v_add_u32_e32 {d}, {last}, {d}")
+                    n += 1
+                    continue
+        out.append(line)
+    return "\n".join(out), n
 
 
 def prio_phases(text):
@@ -114,8 +159,12 @@ def main():
     for name in sys.argv[1:] or ["base", "e64"]:
         s_path = os.path.join(OUT, f"{name}.s")
         if name in DEFINES:
-            compile_s(s_path, DEFINES[name])
+            flags, prio = DEFINES[name]
+            compile_s(s_path, flags)
             n = 0
+            if prio:
+                t, n = prio_phases(open(s_path).read())
+                open(s_path, "w").write(t)
         else:
             t, n = variant(name, text)
             if name != "base":
