@@ -83,6 +83,8 @@ DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
     "prio_w6": (["-DMH_MIN_WAVES=6"], True),
     "prio_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], True),
     "prio_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], True),
+    "grp_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], "sched"),   # more VGPRs, then grouping
+    "grp_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], "sched"),
 }
 
 
@@ -106,13 +108,24 @@ def variant(name, base_text):
         t, n = split_add3(base_text, k)
         t2, n2 = prio_phases(t)
         return t2, n + n2
+    if name.startswith("sched_"):
+        # sched_<D>_<R>: tools/sched_pass.py grouping, then the issue-priority pass
+        from sched_pass import reorder
+        _, dd, rr = name.split("_")
+        t, nb = reorder(base_text, D=int(dd), R=int(rr))
+        t2, n2 = prio_phases(t)
+        return t2, n2
+    if name.startswith("pv_"):
+        # pv_<minF>_<leadF>_<leadH>: marker-placement variants of the issue-priority pass
+        _, mf, lf, lh = name.split("_")
+        return prio_variant(base_text, int(mf), int(lf), int(lh))
     if name.startswith("prio"):
         return prio_phases(base_text)
     raise SystemExit(f"unknown variant {name}")
 
 
 sys.path.insert(0, CSRC)
-from issue_prio import annotate  # noqa: E402
+from issue_prio import annotate, valu_class  # noqa: E402
 
 
 def is_vgpr(op):
@@ -151,6 +164,66 @@ def prio_phases(text):
     return annotate(text)
 
 
+def prio_variant(text, min_f, lead_f, lead_h):
+    """Issue-priority markers with (a) full-rate runs shorter than min_f left at priority 3 and
+    (b) each marker moved lead_f / lead_h VALU instructions earlier (the wave yields, or reclaims,
+    before its head changes class).  Blocks are handled separately (a branch may enter a label)."""
+    lines = text.split("\n")
+    out_marks = {}  # line index -> marker text inserted before it
+    n = 0
+    block = []      # (line index, class) of the current block's VALU instructions
+
+    def flush():
+        nonlocal n
+        if not block:
+            return
+        cls = [c for _, c in block]
+        # runs
+        runs, i = [], 0
+        while i < len(cls):
+            j = i
+            while j < len(cls) and cls[j] == cls[i]:
+                j += 1
+            runs.append([cls[i], i, j])
+            i = j
+        for r in runs:  # short full-rate runs stay in the surrounding half-rate phase
+            if r[0] == "F" and r[2] - r[1] < min_f and len(runs) > 1:
+                r[0] = "H"
+        merged = []
+        for r in runs:
+            if merged and merged[-1][0] == r[0]:
+                merged[-1][2] = r[2]
+            else:
+                merged.append(r)
+        prev_start = -1
+        for c, a, _ in merged:
+            lead = lead_f if c == "F" else lead_h
+            pos = max(prev_start + 1, a - lead) if a > 0 else 0
+            prev_start = pos
+            out_marks[block[pos][0]] = f"\ts_setprio {3 if c == 'H' else 0}"
+            n += 1
+
+    in_kernel = False
+    for k, line in enumerate(lines):
+        if re.match(r"^_Z\S+:", line):
+            flush(); block = []; in_kernel = True
+        elif line.startswith(".Lfunc_end"):
+            flush(); block = []; in_kernel = False
+        elif re.match(r"^\.LBB\w*:", line):
+            flush(); block = []
+        if in_kernel:
+            c = valu_class(line)
+            if c is not None:
+                block.append((k, c))
+    flush()
+    out = []
+    for k, line in enumerate(lines):
+        if k in out_marks:
+            out.append(out_marks[k])
+        out.append(line)
+    return "\n".join(out), n
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     base_s = os.path.join(OUT, "base.s")
@@ -162,7 +235,12 @@ def main():
             flags, prio = DEFINES[name]
             compile_s(s_path, flags)
             n = 0
-            if prio:
+            if prio == "sched":
+                from sched_pass import reorder
+                t, _ = reorder(open(s_path).read(), D=1, R=99)
+                t, n = prio_phases(t)
+                open(s_path, "w").write(t)
+            elif prio:
                 t, n = prio_phases(open(s_path).read())
                 open(s_path, "w").write(t)
         else:
