@@ -85,6 +85,9 @@ DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
     "prio_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], True),
     "grp_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], "sched"),   # more VGPRs, then grouping
     "grp_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], "sched"),
+    # timing-only upper bounds (WRONG results): grouping with register dependencies ignored
+    "ub_grp_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], "ub"),
+    "ub_grp_def": ([], "ub"),
 }
 
 
@@ -235,9 +238,9 @@ def main():
             flags, prio = DEFINES[name]
             compile_s(s_path, flags)
             n = 0
-            if prio == "sched":
+            if prio in ("sched", "ub"):
                 from sched_pass import reorder
-                t, _ = reorder(open(s_path).read(), D=1, R=99)
+                t, _ = reorder(open(s_path).read(), D=1, R=99, raw_only=(prio == "ub"))
                 t, n = prio_phases(t)
                 open(s_path, "w").write(t)
             elif prio:

@@ -42,8 +42,10 @@ def parse(line):
     return m.group(1), regs[0], set(regs[1:])
 
 
-def schedule_segment(items, D, R):
-    """items: list of (line, mnemonic, def, uses).  Returns the reordered lines."""
+def schedule_segment(items, D, R, raw_only=False):
+    """items: list of (line, mnemonic, def, uses).  Returns the reordered lines.  raw_only drops the
+    write-after-read / write-after-write edges: the result is WRONG (registers are reused), only
+    its timing means something -- an upper bound for grouping with register renaming."""
     n = len(items)
     preds = [set() for _ in range(n)]
     last_def, last_uses = {}, {}
@@ -51,9 +53,9 @@ def schedule_segment(items, D, R):
         for u in uses:
             if u in last_def:
                 preds[i].add(last_def[u])          # RAW
-        if d in last_def:
+        if d in last_def and not raw_only:
             preds[i].add(last_def[d])              # WAW
-        for j in last_uses.get(d, ()):
+        for j in (() if raw_only else last_uses.get(d, ())):
             if j != i:
                 preds[i].add(j)                    # WAR
         for u in uses:
@@ -96,7 +98,7 @@ def schedule_segment(items, D, R):
     return [items[i][0] for i in out]
 
 
-def reorder(text, D=2, R=8, min_block=200):
+def reorder(text, D=2, R=8, min_block=200, raw_only=False):
     """Reorder the large basic blocks of the fast_search kernels.  Returns (text, moved blocks)."""
     lines = text.split("\n")
     out, block, nblk = [], [], 0
@@ -113,13 +115,13 @@ def reorder(text, D=2, R=8, min_block=200):
             p = parse(ln)
             if p is None:
                 if seg:
-                    out.extend(schedule_segment(seg, D, R))
+                    out.extend(schedule_segment(seg, D, R, raw_only))
                     seg = []
                 out.append(ln)
             else:
                 seg.append((ln,) + p)
         if seg:
-            out.extend(schedule_segment(seg, D, R))
+            out.extend(schedule_segment(seg, D, R, raw_only))
 
     in_kernel = False
     for ln in lines:
