@@ -231,3 +231,16 @@ def test_profile_counters(gpu):
     assert sum(k["ops"] for k in ks) == p["fast_ops"]
     assert abs(sum(k["ns"] for k in ks) - p["fast_ns"]) <= len(ks)
     assert {(k["word"], k["mode"]) for k in ks} == {(q["word"], q["mode"]) for q in fast}
+
+
+def test_fast_kernels_run_from_the_embedded_module(gpu):
+    """fast_search<J, MODE> runs from the code object embedded in libminehip.so (the issue-priority
+    build): pointing the dev hook at a missing file makes a fast search fail loudly
+    -- nothing falls back to another copy of the kernels -- and the embedded module serves the
+    next search again."""
+    lo = 10 ** 9
+    with env(MINEHIP_DEV_CODE_OBJECT="/nonexistent/fast_search.hsaco"):
+        with pytest.raises(gpu.MinehipError) as e:
+            gpu.search(b"cmu440", lo, lo + (1 << 24) - 1)
+        assert e.value.code == gpu.MH_EHIP
+    assert gpu.search(b"cmu440", lo, lo + 199_999) == oracle.search(b"cmu440", lo, lo + 199_999, threads=4)
