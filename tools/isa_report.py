@@ -1,11 +1,13 @@
 """Per-kernel register use and per-nonce issue cost from the gfx950 assembly.
 
-  make asm && python tools/isa_report.py build/search_kernels.s [filter]
+  make asm && python tools/isa_report.py build/fast_search_prio.s [filter]
 
 For every kernel: VGPRs/SGPRs/scratch from the metadata, and for the
 largest loop body (the per-nonce body of fast_search) the VALU instruction count,
-split into full-rate (1 issue slot) and half-rate (2 slots) instructions as
-measured by tools/valu_ops.hip on MI355X.
+split into full-rate and half-rate instructions as measured by tools/valu_ops.hip
+on MI355X, the issue-priority markers in the loop, and the mix bound: the share
+of the 2-per-quad-cycle issue peak the loop's mix can reach (a half-rate op
+cannot share its quad-cycle with another half-rate op).
 """
 import re
 import sys
@@ -51,7 +53,7 @@ def inner_loop(body):
             ins = []
             for j in range(i, len(lines)):
                 s = lines[j].strip()
-                if s.startswith("v_"):
+                if s.startswith("v_") or s.startswith("s_setprio"):
                     ins.append(s.split()[0])
                 if s.startswith("s_cbranch_scc") or s.startswith("s_branch"):
                     break
@@ -68,7 +70,9 @@ def main():
     for name, body in kernels(text).items():
         if filt not in name:
             continue
-        ins = inner_loop(body)
+        loop = inner_loop(body)
+        marks = sum(1 for x in loop if x == "s_setprio")
+        ins = [x for x in loop if x != "s_setprio"]
         c = Counter(ins)
         half = sum(v for k, v in c.items() if k in HALF_RATE)
         full = len(ins) - half
@@ -76,7 +80,8 @@ def main():
         short = re.sub(r"EvNS_8FastArgsEPNS_7PartialE$", "", name)
         print(f"{short:40s} vgpr={m.get('vgpr_count')} sgpr={m.get('sgpr_count')} "
               f"scratch={m.get('private_segment_fixed_size')} loop_valu={len(ins)} half={half} full={full} "
-              f"slots={2 * half + full}  top={c.most_common(5)}")
+              f"slots={2 * half + full} setprio={marks} "
+              f"mix_bound={len(ins) / (2 * max(half, len(ins) / 2)) if ins else 0:.3f}  top={c.most_common(5)}")
 
 
 if __name__ == "__main__":
