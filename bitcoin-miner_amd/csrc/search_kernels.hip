@@ -163,7 +163,10 @@ hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f) {
     if (it == g_mods.end()) {
         hipModule_t m;
         const hipError_t e = path.empty() ? hipModuleLoadData(&m, mh_fast_co_begin) : hipModuleLoad(&m, path.c_str());
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            (void)hipGetLastError();  // the failure is returned here; do not leave it for the next launch check
+            return e;
+        }
         it = g_mods.emplace(std::make_pair(path, dev), m).first;
     }
     auto fit = g_funcs.find({it->second, J + 16 * mode});
@@ -172,7 +175,10 @@ hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f) {
         snprintf(name, sizeof name, "_ZN2mh11fast_searchILi%dELi%dEEEvNS_8FastArgsEPNS_7PartialE", J, mode);
         hipFunction_t fn;
         const hipError_t e = hipModuleGetFunction(&fn, it->second, name);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return e;
+        }
         fit = g_funcs.emplace(std::make_pair(it->second, J + 16 * mode), fn).first;
     }
     *f = fit->second;
