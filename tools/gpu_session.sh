@@ -138,7 +138,8 @@ for s in $STEPS; do
     lspcfg4)
       # BASELINE configs[4] at its stated size on one GPU: server + 3 GPU miner processes + client
       # over LSP/UDP, 2^42 nonces, one miner SIGKILLed after 5 s; checked against a direct search
-      timeout -k 10 900 python "$ROOT/tools/lsp_cluster_bench.py" --bits 42 --miners 3 --kill 5 \
+      # (LSP_MINERS=8: the configs[4] process layout, eight miner processes, all on the box's one GPU)
+      timeout -k 10 900 python "$ROOT/tools/lsp_cluster_bench.py" --bits 42 --miners ${LSP_MINERS:-3} --kill 5 \
           > "$OUT/lsp_cfg4.json" 2> "$OUT/lsp_cfg4.err"
       rc=$?; echo "lspcfg4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/lsp_cfg4.json"; fatal $rc
       ;;
