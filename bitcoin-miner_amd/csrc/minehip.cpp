@@ -64,7 +64,7 @@ constexpr uint64_t kBatchChunk = 1u << 22;  // nonces per hash_batch transfer
 constexpr int kEventPairs = 512;             // profiled launches buffered before harvesting
 
 struct Timed {
-    hipEvent_t start, stop;
+    hipEvent_t start = nullptr, stop = nullptr;
     int kind;  // 0 fast, 1 generic
     int var;   // fast: kernel variant index (J + 16 * mode)
 };
@@ -127,16 +127,18 @@ int init_locked(DevCtx* c, int dev) {
     MH_HIP(hipGetDeviceProperties(&prop, dev));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(MH_ENODEV, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950 only");
-    MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
-    MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
-    MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
-    MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
-    MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
-    c->pool.resize(kEventPairs);
+    // each resource only once: a call after a failed init (e.g. the code object
+    // did not load) resumes where that one stopped instead of allocating again
+    if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!c->d_partials) MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
+    if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
+    if (!c->h_best) MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
+    if (!c->d_nonces) MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
+    if (!c->d_hashes) MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
+    if (c->pool.empty()) c->pool.resize(kEventPairs);
     for (auto& t : c->pool) {
-        MH_HIP(hipEventCreate(&t.start));
-        MH_HIP(hipEventCreate(&t.stop));
+        if (!t.start) MH_HIP(hipEventCreate(&t.start));
+        if (!t.stop) MH_HIP(hipEventCreate(&t.stop));
     }
     MH_HIP(mh::fast_module_init(dev));  // the fast_search code object (issue-priority build)
     c->dev = dev;
