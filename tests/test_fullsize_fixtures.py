@@ -52,3 +52,31 @@ def test_sample_fixture():
         assert oracle.hash_(b"cmu440", n) == h
     lo, hi, h, n = d["samples"][50]
     assert oracle.search(b"cmu440", lo, hi, threads=os.cpu_count() or 1) == (h, n)
+
+
+def test_config3_fixture():
+    """fullsize_cfg4.json (configs[3] whole, [0, 2^40-1] in 2^32 chunks; gen_cfg4.py): tiles the
+    range, agrees with fullsize_cfg2.json on [0, 2^35) and with every OpenSSL-scanned sample chunk
+    of fullsize_cfg4s.json below 2^40, and re-hashes through the oracle."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_cfg4.json")
+    if not os.path.exists(path):
+        pytest.skip("tests/golden/fullsize_cfg4.json not generated")
+    d = load_golden("fullsize_cfg4.json")
+    assert bytes.fromhex(d["msg_hex"]) == b"cmu440" and d["lo"] == 0 and d["hi"] == (1 << 40) - 1
+    size = 1 << d["chunk_bits"]
+    chunks = [tuple(c) for c in d["chunks"]]
+    assert len(chunks) == (1 << 40) // size and tuple(d["result"]) == min(chunks)
+    for i, (h, n) in enumerate(chunks):
+        assert i * size <= n < (i + 1) * size
+        if i % 17 == 0:
+            assert oracle.hash_(b"cmu440", n) == h
+    d2 = load_golden("fullsize_cfg2.json")
+    per = size >> d2["chunk_bits"]
+    for i in range((1 << 35) // size):
+        assert chunks[i] == min(tuple(c) for c in d2["chunks"][i * per:(i + 1) * per])
+    for lo, hi, h, n in load_golden("fullsize_cfg4s.json")["samples"]:
+        if hi < 1 << 40:
+            c = chunks[lo // size]
+            assert lo // size == hi // size and c <= (h, n)
+            if lo <= c[1] <= hi:
+                assert c == (h, n)
