@@ -32,7 +32,14 @@ for s in $STEPS; do
       make -C "$ROOT" -j16 all > "$OUT/build.log" 2>&1 || { echo "build failed"; exit 1; }
       ;;
     tests)
-      make -C "$ROOT" -q all 2>/dev/null || echo "WARNING: build outputs older than sources" | tee -a "$OUT/session.log"
+      # the box's snapshot carries the built .so files but not build/*.o / *.s (.gpurunignore), so
+      # check the libraries themselves against their sources rather than asking make
+      for f in "$ROOT/bitcoin-miner_amd/minehip/libminehip.so" "$ROOT/oracle/liboracle_sha256.so"; do
+        [ -f "$f" ] || { echo "missing $f: build first (make all)" | tee -a "$OUT/session.log"; exit 1; }
+      done
+      newer=$(find "$ROOT/bitcoin-miner_amd/csrc" "$ROOT/include" -newer "$ROOT/bitcoin-miner_amd/minehip/libminehip.so" \
+              \( -name '*.hip' -o -name '*.cpp' -o -name '*.hpp' -o -name '*.h' -o -name '*.py' \) | head -3)
+      [ -z "$newer" ] || echo "WARNING: sources newer than libminehip.so: $newer" | tee -a "$OUT/session.log"
       timeout -k 10 900 python -u -m pytest "$ROOT/tests" -m gpu -v -x -p no:cacheprovider --timeout 150 \
           --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/pytest_gpu.log"; fatal $rc
