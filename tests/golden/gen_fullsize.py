@@ -18,6 +18,13 @@ Configs (BASELINE.json configs):
          weak-scaling shards at N = 2/4/8 are [0, N*2^32-1], all covered.
   cfg3a  "a" * 100, [0, 2^34-1]: configs[2], host-midstate block.
   cfg3b  "x" * 60,  [0, 2^34-1]: configs[2], two tail blocks.
+  two13, two14, two15, pre0, pre2
+         (b"cmu440-" repeated)[:n] for n = 45, 48, 52, 55, 62, [0, 2^32-1]: the
+         tail layouts BASELINE's messages do not reach at d = 10 -- the last digit
+         in word 13 / 14 / 15 of a tail block that spills into a second block
+         (fast_search<J, kModeTwo>), or in word 0 / 2 of the second tail block
+         (kModePre; cfg3b covers word 1).  The lower buckets of each range go
+         through other layouts (kModeOne, smaller J), all at full size.
   cfg4s  "cmu440", 2^24-nonce samples of configs[3]/[4] ([0, 2^40-1] and
          [0, 2^42-1], digit buckets d = 11..13, too large to scan whole on a
          CPU): 96 seeded random chunks, the chunks straddling 10^11 and
@@ -41,6 +48,9 @@ CONFIGS = {
     "cfg3a": (b"a" * 100, 0, (1 << 34) - 1),
     "cfg3b": (b"x" * 60, 0, (1 << 34) - 1),
 }
+LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62}
+for _name, _n in LAYOUTS.items():
+    CONFIGS[_name] = ((b"cmu440-" * 10)[:_n], 0, (1 << 32) - 1)
 
 
 def build(out_dir="/tmp/minehip_fullsize"):

@@ -10,6 +10,10 @@ reproduce every one of them:
          d = 1..10) and the union of bench.py's weak-scaling shards at 8 GPUs
   cfg3a  "a" x 100 [0, 2^34-1]: configs[2], host-midstate block
   cfg3b  "x" x 60  [0, 2^34-1]: configs[2], two tail blocks
+  two13, two14, two15, pre0, pre2
+         ("cmu440-" repeated)[:n], n = 45/48/52/55/62, [0, 2^32-1]: the d = 10
+         bucket in the two-block layouts fast_search<13..15, Two> and
+         fast_search<0, Pre>, <2, Pre> (cfg3b is <1, Pre>), lower buckets in others
   cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
   cfg4   "cmu440" [0, 2^40-1]: configs[3] whole, its 256 2^32-chunk minima
          (tests/golden/gen_cfg4.py: SHA-NI scan, checked against OpenSSL)
@@ -26,7 +30,7 @@ from test_gpu_parity import env
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ("cfg2", "cfg3a", "cfg3b")
+CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2")
 
 
 def fixture(name):
@@ -80,6 +84,17 @@ def test_plan_knobs_full_size(gpu):
                dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0)):
         with env(**kv):
             assert gpu.search(msg, 0, (1 << 32) - 1) == exp, kv
+
+
+@pytest.mark.parametrize("name", ("two15", "pre0"))
+def test_plan_knobs_two_block_layouts(gpu, name):
+    """The two-block layouts at 2^32 under other lane run lengths, launch sizes and with every
+    bucket on the fast kernels: the answer stays the fixture's."""
+    msg, lo, hi, _, result, _ = fixture(name)
+    for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1 << 18),
+               dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0)):
+        with env(**kv):
+            assert gpu.search(msg, lo, hi) == result, kv
 
 
 def test_search_multi_full_size(gpu):
