@@ -25,6 +25,10 @@ Configs (BASELINE.json configs):
          (fast_search<J, kModeTwo>), or in word 0 / 2 of the second tail block
          (kModePre; cfg3b covers word 1).  The lower buckets of each range go
          through other layouts (kModeOne, smaller J), all at full size.
+  pre3, pre4, top
+         2^32 nonces from 10^13 / 10^17 for the 62-byte message (the 14- and
+         18-digit buckets: fast_search<3, Pre>, <4, Pre>), and "cmu440" over
+         [2^64-2^32, 2^64-1] (20 digits, fast_search<6, One>, up to the last u64).
   cfg4s  "cmu440", 2^24-nonce samples of configs[3]/[4] ([0, 2^40-1] and
          [0, 2^42-1], digit buckets d = 11..13, too large to scan whole on a
          CPU): 96 seeded random chunks, the chunks straddling 10^11 and
@@ -51,6 +55,9 @@ CONFIGS = {
 LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62}
 for _name, _n in LAYOUTS.items():
     CONFIGS[_name] = ((b"cmu440-" * 10)[:_n], 0, (1 << 32) - 1)
+CONFIGS["pre3"] = ((b"cmu440-" * 10)[:62], 10 ** 13, 10 ** 13 + (1 << 32) - 1)
+CONFIGS["pre4"] = ((b"cmu440-" * 10)[:62], 10 ** 17, 10 ** 17 + (1 << 32) - 1)
+CONFIGS["top"] = (b"cmu440", (1 << 64) - (1 << 32), (1 << 64) - 1)
 
 
 def build(out_dir="/tmp/minehip_fullsize"):

@@ -17,19 +17,28 @@ CFGS = {"cfg2": (b"cmu440", (1 << 35) - 1), "cfg3a": (b"a" * 100, (1 << 34) - 1)
 # tail layouts of the d = 10 bucket that BASELINE's messages do not reach (gen_fullsize.py)
 LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62}
 CFGS.update({k: ((b"cmu440-" * 10)[:n], (1 << 32) - 1) for k, n in LAYOUTS.items()})
+# (msg, hi, lo) for the ranges that do not start at 0: the 14-/18-digit buckets and the top of u64
+CFGS.update({"pre3": ((b"cmu440-" * 10)[:62], 10 ** 13 + (1 << 32) - 1, 10 ** 13),
+             "pre4": ((b"cmu440-" * 10)[:62], 10 ** 17 + (1 << 32) - 1, 10 ** 17),
+             "top": (b"cmu440", (1 << 64) - 1, (1 << 64) - (1 << 32))})
+
+
+def _cfg(name):
+    msg, hi, *lo = CFGS[name]
+    return msg, (lo[0] if lo else 0), hi
 
 
 @pytest.mark.parametrize("name", sorted(CFGS))
 def test_fixture_consistent(name):
     d = load_golden(f"fullsize_{name}.json")
-    msg, hi = CFGS[name]
-    assert bytes.fromhex(d["msg_hex"]) == msg and d["lo"] == 0 and d["hi"] == hi
+    msg, lo, hi = _cfg(name)
+    assert bytes.fromhex(d["msg_hex"]) == msg and d["lo"] == lo and d["hi"] == hi
     chunks = [tuple(c) for c in d["chunks"]]
     size = 1 << d["chunk_bits"]
-    assert len(chunks) == (hi + 1) // size
+    assert len(chunks) == (hi - lo + 1) // size
     assert tuple(d["result"]) == min(chunks)
     for i, (h, n) in enumerate(chunks):
-        assert i * size <= n < (i + 1) * size
+        assert lo + i * size <= n < lo + (i + 1) * size
         if i % 97 == 0:
             assert oracle.hash_(msg, n) == h
 
@@ -37,10 +46,10 @@ def test_fixture_consistent(name):
 @pytest.mark.parametrize("name", sorted(CFGS))
 def test_fixture_chunk_vs_oracle(name):
     d = load_golden(f"fullsize_{name}.json")
-    msg, _ = CFGS[name]
+    msg, lo, _ = _cfg(name)
     size = 1 << d["chunk_bits"]
-    i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000}.get(name, 255)  # d = 10, 11, 11, 10 chunks
-    got = oracle.search(msg, i * size, (i + 1) * size - 1, threads=os.cpu_count() or 1)
+    i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000}.get(name, 255)  # cfg*: d = 10, 11, 11 chunks; the rest: last
+    got = oracle.search(msg, lo + i * size, lo + (i + 1) * size - 1, threads=os.cpu_count() or 1)
     assert got == tuple(d["chunks"][i])
 
 

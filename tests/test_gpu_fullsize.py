@@ -14,6 +14,9 @@ reproduce every one of them:
          ("cmu440-" repeated)[:n], n = 45/48/52/55/62, [0, 2^32-1]: the d = 10
          bucket in the two-block layouts fast_search<13..15, Two> and
          fast_search<0, Pre>, <2, Pre> (cfg3b is <1, Pre>), lower buckets in others
+  pre3, pre4, top
+         2^32 nonces from 10^13 and 10^17 for the 62-byte message (<3, Pre>, <4, Pre>),
+         and "cmu440" over [2^64-2^32, 2^64-1] (20 digits, <6, One>, up to the last u64)
   cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
   cfg4   "cmu440" [0, 2^40-1]: configs[3] whole, its 256 2^32-chunk minima
          (tests/golden/gen_cfg4.py: SHA-NI scan, checked against OpenSSL)
@@ -30,7 +33,7 @@ from test_gpu_parity import env
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2")
+CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2", "pre3", "pre4", "top")
 
 
 def fixture(name):
