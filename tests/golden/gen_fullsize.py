@@ -25,6 +25,11 @@ Configs (BASELINE.json configs):
          (fast_search<J, kModeTwo>), or in word 0 / 2 of the second tail block
          (kModePre; cfg3b covers word 1).  The lower buckets of each range go
          through other layouts (kModeOne, smaller J), all at full size.
+  one1, one5, one7, one8, one10, one12
+         (b"cmu440-" repeated)[:n] for n = 0, 13, 21, 25, 30, 41, [0, 2^32-1]: one tail
+         block, the d = 7..10 buckets in fast_search<1|2|5|7|8|9|10|12, One>; with
+         cfg2 (<3>, <4>), cfg3a (<11>), two13's lower buckets (<13>) and top (<6>)
+         every layout the default plan sends to the fast kernels has a fixture
   pre3, pre4, top
          2^32 nonces from 10^13 / 10^17 for the 62-byte message (the 14- and
          18-digit buckets: fast_search<3, Pre>, <4, Pre>), and "cmu440" over
@@ -54,6 +59,8 @@ CONFIGS = {
 }
 LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62}
 for _name, _n in LAYOUTS.items():
+    CONFIGS[_name] = ((b"cmu440-" * 10)[:_n], 0, (1 << 32) - 1)
+for _name, _n in {"one1": 0, "one5": 13, "one7": 21, "one8": 25, "one10": 30, "one12": 41}.items():
     CONFIGS[_name] = ((b"cmu440-" * 10)[:_n], 0, (1 << 32) - 1)
 CONFIGS["pre3"] = ((b"cmu440-" * 10)[:62], 10 ** 13, 10 ** 13 + (1 << 32) - 1)
 CONFIGS["pre4"] = ((b"cmu440-" * 10)[:62], 10 ** 17, 10 ** 17 + (1 << 32) - 1)

@@ -15,7 +15,8 @@ from oracle import oracle
 CFGS = {"cfg2": (b"cmu440", (1 << 35) - 1), "cfg3a": (b"a" * 100, (1 << 34) - 1),
         "cfg3b": (b"x" * 60, (1 << 34) - 1)}
 # tail layouts of the d = 10 bucket that BASELINE's messages do not reach (gen_fullsize.py)
-LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62}
+LAYOUTS = {"two13": 45, "two14": 48, "two15": 52, "pre0": 55, "pre2": 62,
+           "one1": 0, "one5": 13, "one7": 21, "one8": 25, "one10": 30, "one12": 41}
 CFGS.update({k: ((b"cmu440-" * 10)[:n], (1 << 32) - 1) for k, n in LAYOUTS.items()})
 # (msg, hi, lo) for the ranges that do not start at 0: the 14-/18-digit buckets and the top of u64
 CFGS.update({"pre3": ((b"cmu440-" * 10)[:62], 10 ** 13 + (1 << 32) - 1, 10 ** 13),
@@ -92,3 +93,19 @@ def test_config3_fixture():
             assert lo // size == hi // size and c <= (h, n)
             if lo <= c[1] <= hi:
                 assert c == (h, n)
+
+
+def test_fixtures_cover_every_fast_layout():
+    """The default plans of the full-size fixtures' ranges (host-only mh_plan) use every
+    fast_search<J, MODE> instantiation the default plan can ever choose: all 22 but <0, One>,
+    whose last digit would sit in message bytes 0..3, i.e. d <= 4 -- always a bucket of fewer
+    than 2^20 nonces, which goes to the generic kernel."""
+    import minehip
+    used = set()
+    for name in CFGS:
+        msg, lo, hi = _cfg(name)
+        used |= {(p["word"], p["mode"]) for p in minehip.plan(msg, lo, hi) if p["kind"] == 0}
+    for lo, hi, _, _ in load_golden("fullsize_cfg4s.json")["samples"]:
+        used |= {(p["word"], p["mode"]) for p in minehip.plan(b"cmu440", lo, hi) if p["kind"] == 0}
+    every = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(j, 2) for j in (13, 14, 15)}
+    assert used == every - {(0, 0)}, sorted(every - used)

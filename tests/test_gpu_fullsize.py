@@ -14,6 +14,10 @@ reproduce every one of them:
          ("cmu440-" repeated)[:n], n = 45/48/52/55/62, [0, 2^32-1]: the d = 10
          bucket in the two-block layouts fast_search<13..15, Two> and
          fast_search<0, Pre>, <2, Pre> (cfg3b is <1, Pre>), lower buckets in others
+  one1, one5, one7, one8, one10, one12
+         ("cmu440-" repeated)[:n], n = 0/13/21/25/30/41, [0, 2^32-1]: one tail block,
+         d = 7..10 in <1|2|5|7|8|9|10|12, One>; with the rest every layout the
+         default plan uses (test_fullsize_fixtures.py checks the coverage)
   pre3, pre4, top
          2^32 nonces from 10^13 and 10^17 for the 62-byte message (<3, Pre>, <4, Pre>),
          and "cmu440" over [2^64-2^32, 2^64-1] (20 digits, <6, One>, up to the last u64)
@@ -33,7 +37,8 @@ from test_gpu_parity import env
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2", "pre3", "pre4", "top")
+CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2", "pre3", "pre4", "top",
+        "one1", "one5", "one7", "one8", "one10", "one12")
 
 
 def fixture(name):
