@@ -135,6 +135,14 @@ def test_golden_expect_covers_every_bench_range():
         assert bench.golden_expect(c["msg"].encode(), 0, (1 << c["bits"]) - 1) is not None
     assert bench.golden_expect(b"no fixture", 0, 99) is None
     assert bench.golden_expect(MSG, 5, 1 << 33) is None  # not chunk-aligned
+    # the N > 1 default (configs[3], strong): the timed region's merged range is [0, 2^40-1],
+    # answered by the whole-range fixture, so the driver's 2/4/8-GPU lines carry golden_ok
+    c4 = bench.CONFIGS["4"]
+    for world in (2, 4, 8):
+        lo = bench.job_range(c4, world, 0, 20)[0]
+        hi = bench.job_range(c4, world, 19, 20)[1]
+        assert (lo, hi) == (0, (1 << 40) - 1)
+        assert bench.golden_expect(MSG, lo, hi) == (26475375, 32018601659), world
 
 
 def _run_bench(args, env_extra=None):
