@@ -274,7 +274,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         L = std::min(L, 5);
         // A lane runs 10^L nonces serially: a bucket with few runs would leave
         // most SIMDs idle and end in a long tail, so shorten the runs until
-        // the bucket has min_lanes of them (2^23: ~32 workgroups per CU).
+        // the bucket has min_lanes of them (2^21: ~8 workgroups per CU).
         while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
         FastArgs fa;
         int J = 0, mode = 0, nb = 1;

@@ -47,13 +47,16 @@ struct Piece {
 };
 
 struct PlanOpts {
-    // L <= 2 and >= 2^23 runs per bucket: launches of up to 65,536 workgroups
-    // (~32 per CU) instead of the ~13k that L = 3 gives a 2^32-nonce launch;
-    // the shorter tail of a bigger launch outweighs the per-run work done 10x
-    // more often (+1.2% on configs[1], +0.9% on 100 x 'a').
-    int lower_digits = 2;                        // L upper bound (nonces per lane = 10^L)
-    uint64_t min_lanes = 1u << 23;               // lower L until a bucket has this many runs
-    uint64_t max_nonces_per_launch = 1ull << 32; // bounds one launch to ~0.1 s
+    // L <= 3 with >= 2^21 runs per bucket and up to 2^34 nonces (~67k workgroups
+    // at L = 3) per launch.  With the issue-priority build the per-run work
+    // (digit formatting, hoisted rounds, the first-nonce candidate scan, wave
+    // start and the workgroup reduction) costs more than the longer tail of
+    // 1,000-nonce lanes: +2% on configs[1], +5% / +4% on configs[2]'s halves,
+    // +3% on configs[3] against L <= 2, 2^23 runs, 2^32-nonce launches, the
+    // round-1 choice (profiles/r02ap_kbench_plan.json).
+    int lower_digits = 3;                        // L upper bound (nonces per lane = 10^L)
+    uint64_t min_lanes = 1u << 21;               // lower L until a bucket has this many runs
+    uint64_t max_nonces_per_launch = 1ull << 34; // one launch <= ~0.35 s (one tail block) / ~0.6 s (two)
     uint32_t max_blocks = 1u << 17;              // workgroups per launch (<= kMaxBlocksPerLaunch; +0.1% over 2^16)
     uint64_t generic_below = 1u << 20;           // a bucket this small goes to the generic kernel whole
 };

@@ -141,8 +141,16 @@ def test_plan_coalesces_small_buckets():
 
 
 def test_plan_launch_cap():
+    """PlanOpts: at most 2^34 nonces and 131,072 workgroups of 256 lanes per fast launch, and
+    configs[3]'s big buckets run 1,000-nonce lanes (L = 3) in launches near the nonce cap."""
     pieces = check_plan(b"cmu440", 0, 2 ** 40 - 1)
-    assert max(p["count"] for p in pieces) <= 2 ** 32
+    fast = [p for p in pieces if p["kind"] == 0]
+    assert max(p["count"] for p in pieces) <= 2 ** 34
+    for p in fast:
+        assert -(-(p["count"] // 10 ** p["lo_digits"]) // 256) <= 131072
+    big = [p for p in fast if p["digits"] >= 11]
+    assert big and all(p["lo_digits"] == 3 for p in big)
+    assert max(p["count"] for p in big) > 2 ** 33
 
 
 # ---- bitcoin.Message codec (Go encoding/json bytes) ------------------------
