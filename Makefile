@@ -24,7 +24,9 @@ BIN     := $(PKG)/bin
 CLIS    := $(BIN)/minehip-search $(BIN)/minehip-miner $(BIN)/minehip-server $(BIN)/minehip-client
 RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
-all: $(LIB) $(LSPLIB) $(CLIS) oracle
+DEVLIB  := $(BUILD)/dev/libminehip.so
+
+all: $(LIB) $(LSPLIB) $(CLIS) oracle dev
 
 # LSP endpoint (host only, wire compatible with the reference's Go lsp package)
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
@@ -32,6 +34,14 @@ $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
 
 $(LIB): $(SRCS) $(HDRS) $(FAST_O)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -x none $(FAST_O)
+
+# dev build: the same library plus the experiment / test hooks (MINEHIP_DEV_CODE_OBJECT,
+# MINEHIP_DEV_LDS, MINEHIP_TEST_FAIL_WORKER).  Never the package's library: tools and the
+# tests that need a hook load it explicitly (MINEHIP_LIB=build/dev/libminehip.so).
+dev: $(DEVLIB)
+$(DEVLIB): $(SRCS) $(HDRS) $(FAST_O)
+	mkdir -p $(BUILD)/dev
+	$(HIPCC) $(HIPFLAGS) -DMH_DEV_HOOKS -shared -o $@ $(SRCS) -x none $(FAST_O)
 
 # fast_search<J, MODE>: gfx950 assembly -> issue-priority pass (s_setprio around half-/full-rate
 # runs) -> code object -> embedded in the library (fast_co.S)
@@ -83,7 +93,7 @@ build/valu_%: tools/valu_%.hip
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 clean:
-	rm -f $(LIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_PS) $(FAST_CO) $(FAST_O) $(BUILD)/fast_search_prio.o
+	rm -f $(LIB) $(DEVLIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_PS) $(FAST_CO) $(FAST_O) $(BUILD)/fast_search_prio.o
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle asm clean probes
+.PHONY: all oracle asm clean probes dev

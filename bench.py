@@ -29,13 +29,16 @@ shard, merged on the host):
     merges on the host).  Fewer than N visible devices is an error: exit 2, no
     JSON line.  `--multi` forces this path at N = 1.
 
-Rank 0 prints ONE JSON line.  `roofline` is priced on SURVEY §8(d) D4's
-algorithmic basis (1,616 int32 VALU ops per SHA-256 compression x tail blocks
-per nonce) over the dominant kernel's HIP-event launch time, against the VALU
-peak 256 CU x 128 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: 4 SIMD-32 per CU);
-`roofline.issue` is the same kernel's instruction issue against 2 VALU instructions
-per SIMD quad-cycle.  At N = 1, rocprofv3 --pmc passes over one launch of
-each of the two largest kernels give HBM traffic and the SQ counters
+Rank 0 prints ONE JSON line.  `roofline.frac` is the dominant kernel's
+algorithmic per-nonce work (nonce_ops: the VALU instructions one nonce needs
+after hoisting, SURVEY §8(d) D4 restated for gfx950) x nonces over its
+HIP-event launch time, against the VALU issue peak: 2 instructions per SIMD
+quad-cycle = 256 CU x 128 lanes/clk x 2.4 GHz.  It cannot
+exceed 1.  `roofline.frac_survey_d4` prices a nonce at SURVEY D4's 1,616 ops
+per compression instead (can exceed 1).  `roofline.resources` are the kernel's
+VGPR/SGPR/scratch from the embedded code object.  At N = 1, rocprofv3 --pmc
+passes over one launch of each of the two largest kernels give HBM traffic,
+the clock (`sclk_ghz`, `roofline.frac_at_sclk`) and the SQ counters
 (`roofline.pmc`).  `cpu_baseline` times the CPU port of the reference loop
 (oracle/) on a bounded sample, at N = 1 only.
 """
@@ -354,63 +357,80 @@ def kernel_totals(per_dev_kstats):
     return sorted(tot.values(), key=lambda k: -k["ns"])
 
 
-def roofline(kst, cus, n_devices):
+def roofline(kst, cus, n_devices, resources=None):
     """Roofline of the dominant kernel from its HIP-event launch times (summed
-    over devices, so achieved is per GPU).  frac is on SURVEY §8(d) D4's
-    algorithmic basis; issue counts the instructions its compiled loop issues."""
+    over devices, so achieved is per GPU).
+
+    frac: the algorithm's per-nonce work over the VALU issue peak.  The work is
+    nonce_ops (plan.cpp nonce_cost, exported per piece by mh_plan): the VALU
+    instructions one nonce's SHA-256 needs once the rounds and schedule words
+    shared by a lane's nonces are hoisted -- SURVEY §8(d) D4 restated for
+    gfx950 (v_bitop3 xor3).  The kernel issues at least that many
+    instructions per nonce (PMC SQ_INSTS_VALU: 1,200.6 for fast_search<4,0>
+    against nonce_ops 1,195), so frac <= the hardware's issue fraction <= 1.
+    frac_survey_d4 prices every nonce at SURVEY D4's 1,616 ops x tail blocks:
+    a pricing convention that credits the hoisting and can exceed 1."""
     peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
     if not kst:
         return {"bound": "valu", "achieved": None, "peak": round(peak, 3), "frac": None}
     dom = kst[0]
     blocks = 1 if dom["mode"] == 0 else 2       # tail blocks hashed per nonce (Pre/Two: 2)
     sec = dom["ns"] * 1e-9
+    nonces = max(1, dom["nonces"])
     ghs = dom["nonces"] / sec / 1e9
-    alg = dom["nonces"] * SURVEY_OPS_PER_COMPRESSION * blocks  # int32 ops, §8(d) D4
-    achieved = alg / sec / 1e12
-    ops = dom["ops"]                             # lane-instructions of the per-nonce loops
-    n_instr = dom["ops"] / max(1, dom["nonces"])
-    n_half = (dom["slots"] - dom["ops"]) / max(1, dom["nonces"])  # slots count a half-rate op twice
+    ops = dom["ops"]                             # nonces x nonce_ops of every launch
+    n_instr = ops / nonces
+    n_half = (dom["slots"] - dom["ops"]) / nonces  # slots count a half-rate op twice
+    achieved = ops / sec / 1e12
+    mix = n_instr / (2 * max(n_half, n_instr / 2))
+    d4 = dom["nonces"] * SURVEY_OPS_PER_COMPRESSION * blocks
     launches = max(1, dom["launches"])
     line = {
         "bound": "valu",
         "achieved": round(achieved, 3),
         "peak": round(peak, 3),
-        "unit": "T int32 VALU ops/s per GPU",
+        "unit": "T int32 VALU lane-instructions/s per GPU",
         "frac": round(achieved / peak, 4),
-        "frac_alg": round(achieved / peak, 4),
-        "basis": f"SURVEY §8(d) D4: {SURVEY_OPS_PER_COMPRESSION} ops per compression x {blocks} tail block(s) "
-                 f"per nonce over the dominant kernel's HIP-event launch time; peak {cus} CU x "
-                 f"{LANES_PER_CU_CLK} lanes/clk x {PEAK_SCLK_HZ / 1e9} GHz",
-        "frac_note": "D4 prices a nonce at full compressions; the loop hoists the work shared by a "
-                     "lane's nonces and issues fewer instructions, so this fraction credits the hoisting "
-                     "and can exceed 1.  The hardware fraction is issue.frac.",
+        "frac_at_sclk": None,                    # against the peak at the clock the kernel ran at (PMC)
+        "basis": "algorithmic work per nonce = nonce_ops, the VALU instructions one nonce's SHA-256 "
+                 "needs after hoisting the work a lane's nonces share (SURVEY §8(d) D4 restated for "
+                 "gfx950, DESIGN.md §4), x the dominant kernel's nonces / its HIP-event launch time; "
+                 f"peak = {cus} CU x 4 SIMD x 2 VALU instructions per quad-cycle x 64 lanes / 4 "
+                 f"(= {LANES_PER_CU_CLK} lane-instructions/clk/CU) x {PEAK_SCLK_HZ / 1e9} GHz",
+        "alg_instr_per_nonce": round(n_instr, 1),
+        "half_rate_per_nonce": round(n_half, 1),
+        # a half-rate op cannot share its quad-cycle with another half-rate op, so a nonce needs
+        # >= max(H, N/2) quad-cycles: the most this per-nonce mix can reach
+        "mix_bound_frac": round(mix, 4),
+        "frac_of_mix_bound": round(achieved / peak / mix, 4),
+        "frac_survey_d4": round(d4 / sec / 1e12 / peak, 4),
+        "frac_survey_d4_note": f"SURVEY §8(d) D4's {SURVEY_OPS_PER_COMPRESSION} ops per compression x "
+                               f"{blocks} tail block(s) per nonce over the same time and peak: D4 prices "
+                               "a nonce at full compressions, the kernel hoists what a lane's nonces "
+                               "share, so this ratio credits the hoisting and can exceed 1",
         "kernel": dom["name"],
         "tail_blocks": blocks,
         "launches": dom["launches"],
         "devices": n_devices,
         "avg_launch_ms": round(dom["ns"] / launches / 1e6, 4),
         "nonces_per_launch": dom["nonces"] // launches,
-        "alg_ops_per_launch": alg // launches,
+        "alg_instr_per_launch": ops // launches,
         "kernel_ghs": round(ghs, 4),
-        # VALU issue: one instruction per SIMD quad-cycle, two when the second is full rate (a
-        # full-rate op beside a half-rate or full-rate one; DESIGN.md §4) -> peak 2 per quad =
-        # 128 lane-instructions/clk/CU, the same 78.64 T.  A nonce is one lane, so lane-instructions/s
-        # = nonces/s x instructions per nonce.  The mix bound: a half-rate op cannot share its
-        # quad-cycle with another half-rate op, so a nonce needs >= max(H, N/2) quad-cycles.
-        "issue": {
-            "achieved": round(ops / sec / 1e12, 3), "peak": round(peak, 3), "frac": round(ops / sec / 1e12 / peak, 4),
-            "instr_per_nonce": round(n_instr, 1), "half_rate_per_nonce": round(n_half, 1),
-            "mix_bound_frac": round(n_instr / (2 * max(n_half, n_instr / 2)), 4),
-            "note": "lane-instructions/s of the compiled per-nonce loop (hoisted run/group work excluded) "
-                    "against 2 VALU instructions per SIMD quad-cycle; mix_bound_frac = the most this "
-                    "loop's half-/full-rate mix can reach"},
         "full_compression_instr": OPS_PER_BLOCK,
     }
+    if resources:
+        r = resources.get((dom["word"], dom["mode"]))
+        if r:
+            line["resources"] = dict(r, source="NT_AMDGPU_METADATA of the code object embedded in "
+                                               "libminehip.so (minehip/codeobj.py)")
     if len(kst) > 1:
         s = kst[1]
         line["second_kernel"] = {"kernel": s["name"], "ms": round(s["ns"] / 1e6, 3),
                                  "kernel_ghs": round(s["nonces"] / (s["ns"] * 1e-9) / 1e9, 4),
-                                 "instr_per_nonce": round(s["ops"] / max(1, s["nonces"]), 1)}
+                                 "alg_instr_per_nonce": round(s["ops"] / max(1, s["nonces"]), 1),
+                                 "frac": round(s["ops"] / (s["ns"] * 1e-9) / 1e12 / peak, 4)}
+        if resources and resources.get((s["word"], s["mode"])):
+            line["second_kernel"]["resources"] = resources[(s["word"], s["mode"])]
     return line
 
 
@@ -528,7 +548,8 @@ def main():
     props = torch.cuda.get_device_properties(devs[0])
     cus = int(props.multi_processor_count)
     kst = kernel_totals([p["kstats"] for p in per_dev])
-    roof = roofline(kst, cus, len(per_dev))
+    from minehip import codeobj
+    roof = roofline(kst, cus, len(per_dev), codeobj.fast_kernel_resources())
     # algorithmic bytes of the dominant launch: one 16-byte (hash, nonce) partial per 256-lane workgroup
     job_lo, job_hi = job_range(cfg, n_gpus, 0, 1 if cfg["scaling"] == "weak" else steps)
     my_lo, my_hi = (rank_range(cfg, rank, world, 0, steps) if launched else (job_lo, job_hi))
@@ -556,11 +577,13 @@ def main():
                                     f"WRITE_SIZE {v0['WRITE_SIZE']:.2f} KiB")
             roof["pmc"] = pmc_derived(v0, pieces[0], cus)
             roof["pmc"]["kernel"] = kst[0]["name"]
-            # achieved / frac again at the clock this launch ran at
+            # frac again against the peak at the clock this launch ran at
             at = roof["pmc"]["sclk_ghz"] * 1e9
-            roof["pmc"]["frac_alg_at_sclk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
-            roof["pmc"]["issue_frac_at_sclk"] = round(roof["issue"]["achieved"]
-                                                      / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+            roof["frac_at_sclk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+            roof["sclk_ghz"] = roof["pmc"]["sclk_ghz"]
+            # what the hardware issued (PMC), against the same peak: >= frac, since the kernel issues
+            # at least nonce_ops instructions per nonce
+            roof["pmc"]["issued_frac_at_sclk"] = round(2 / roof["pmc"]["cycles_per_valu_instr"], 4)
             if len(pieces) > 1:
                 v1 = vals[f"fast_search<{pieces[1]['word']}, {pieces[1]['mode']}>"]
                 roof["second_kernel"]["pmc"] = pmc_derived(v1, pieces[1], cus)
@@ -588,6 +611,10 @@ def main():
             "steps": steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_max / steps * 1e3, 3),
+            # engine clock of the dominant kernel (PMC pass at N = 1; None otherwise): MI355X runs
+            # this VALU-bound kernel at its package power limit, so the clock, and with it value,
+            # differs from box to box
+            "sclk_ghz": roof.get("sclk_ghz"),
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,

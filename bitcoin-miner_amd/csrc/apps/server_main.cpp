@@ -16,6 +16,33 @@
 #include "../../../include/minehip_server.h"
 #include "common.hpp"
 
+namespace {
+
+// Upper bound of the LSP Data datagram that carries an n-byte payload: base64
+// plus the JSON of lsp.Message with the largest ConnID / SeqNum / Size
+// (lsp/message.go:17-24; {"Type":1,"ConnID":..,"SeqNum":..,"Size":..,"Payload":".."}).
+size_t frame_bound(size_t n) { return 4 * ((n + 2) / 3) + 128; }
+
+// A client Request is re-encoded for each miner chunk with other bounds (up to
+// 20 digits each) and the server's own JSON escaping (Go's: <, >, & and control
+// bytes as \u00XX, invalid UTF-8 as U+FFFD), so a Request that reached the
+// server in one datagram need not fit in one as a miner Request.  Such a
+// Request is refused up front: otherwise every chunk write would fail with
+// LSP_ETOOBIG and the client would wait forever.
+constexpr int64_t kRequest = 1;  // MsgType Request (message.go:9-13)
+
+bool miner_request_fits(const uint8_t* payload, size_t n, std::vector<uint8_t>& scratch) {
+    mh_message m;
+    scratch.resize(3 * n + 16);  // an invalid UTF-8 byte decodes to U+FFFD, 3 bytes
+    if (mh_msg_decode((const char*)payload, n, &m, scratch.data(), scratch.size()) != MH_OK || m.type != kRequest)
+        return true;  // not a Request: the server loop decides what to do with it
+    size_t need = 0;
+    mh_msg_encode(kRequest, scratch.data(), m.data_len, UINT64_MAX, UINT64_MAX, 0, 0, nullptr, 0, &need);
+    return frame_bound(need) <= LSP_MAX_DATAGRAM;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
     if (argc != 2) {
         printf("Usage: ./%s <port>", argv[0]);  // server.go:42-45
@@ -48,6 +75,7 @@ int main(int argc, char** argv) {
 
     std::vector<uint8_t> buf(1 << 16);
     std::vector<char> out(1 << 16);
+    std::vector<uint8_t> scratch;
     for (;;) {
         int conn = 0;
         size_t n = 0;
@@ -60,7 +88,11 @@ int main(int argc, char** argv) {
         if (r == LSP_OK) {
             // a refused Request gets no Result: close that client, which then prints
             // Disconnected; other bad payloads are ignored
-            if (mh_server_read(v, conn, (const char*)buf.data(), n, now) == MH_EREJECTED) {
+            if (!miner_request_fits(buf.data(), n, scratch)) {
+                fprintf(stderr, "minehip-server: conn %d: Request too large to forward to a miner in one "
+                        "LSP datagram; refused\n", conn);
+                lsp_server_close_conn(s, conn);
+            } else if (mh_server_read(v, conn, (const char*)buf.data(), n, now) == MH_EREJECTED) {
                 fprintf(stderr, "minehip-server: conn %d: %s\n", conn, mh_last_error());
                 lsp_server_close_conn(s, conn);
             }
@@ -82,7 +114,15 @@ int main(int argc, char** argv) {
                 continue;
             }
             if (k != 1) break;
-            lsp_server_write(s, (int)wc, (const uint8_t*)out.data(), wn);  // a lost conn surfaces via Read
+            // a lost conn surfaces via Read; a frame too large for one datagram cannot happen for a
+            // Request that passed miner_request_fits, but if it does, that miner can never get this
+            // chunk: drop it as lost, so its chunk goes back to the job instead of hanging it
+            if (lsp_server_write(s, (int)wc, (const uint8_t*)out.data(), wn) == LSP_ETOOBIG) {
+                fprintf(stderr, "minehip-server: conn %d: write of %zu bytes exceeds one LSP datagram; "
+                        "dropping the connection\n", (int)wc, wn);
+                mh_server_lost(v, wc, now);
+                lsp_server_close_conn(s, (int)wc);
+            }
         }
     }
     mh_server_destroy(v);

@@ -204,9 +204,6 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
-#if defined(MH_SYNC) && MH_SYNC == 10
-        __builtin_amdgcn_s_barrier();
-#endif
         // digits 0..L-2 of q = 10*g + i: wave-uniform, so this is SALU work
         uint32_t cj = 0u, cjm = 0u, gq = g;
         for (uint32_t k = a.L - 1u; k-- > 0u;) {
@@ -243,9 +240,6 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 
         for (uint32_t i = 0; i < 10u; ++i) {
             // ---- per nonce ------------------------------------------------
-#if defined(MH_SYNC) && MH_SYNC == 1
-            __builtin_amdgcn_s_barrier();
-#endif
             const uint32_t inc = i << sh_last;  // SALU
             const uint32_t s0inc = kIncSigma.s0[sh_last >> 3][i], s1inc = kIncSigma.s1[sh_last >> 3][i];
             uint32_t x[64];

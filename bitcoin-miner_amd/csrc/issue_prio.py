@@ -20,26 +20,23 @@ issue beside their half-rate ones: the SHA-256 round mix goes from 4.07 to
 s_setprio is a scalar instruction (it changes the wave's own arbitration
 priority only; no memory, no data).
 """
+import os
 import re
 import sys
 
-# gfx950 VALU ops that issue at half rate (wave64 in 4 cycles), measured by
-# tools/valu_ops.hip (profiles/r01d_valu_ops.json) and tools/gen_valu_bank.py
-HALF_RATE = {
-    "v_alignbit_b32", "v_alignbyte_b32", "v_add3_u32", "v_xad_u32", "v_bfi_b32", "v_lshl_or_b32",
-    "v_lshl_add_u32", "v_add_lshl_u32", "v_and_or_b32", "v_or3_b32", "v_perm_b32", "v_cndmask_b32_e64",
-    "v_mad_u32_u24", "v_lshrrev_b64", "v_lshlrev_b64", "v_mov_b64", "v_lshlrev_b32_e64",
-    "v_lshrrev_b32_e64", "v_mad_u64_u32", "v_pk_add_u16",
-}
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from valu_rates import UnknownOpcode, valu_rate  # noqa: E402  (the opcode tables)
+
 PRIO_HALF, PRIO_FULL = 3, 0
 
 
 def valu_class(line):
+    """'H' / 'F' for a VALU instruction line, None for any other line;
+    UnknownOpcode for a VALU opcode valu_rates.py does not list."""
     m = re.match(r"^\s+(v_\w+)", line)
     if not m:
         return None
-    op = m.group(1)
-    return "H" if op in HALF_RATE or op.removesuffix("_e64") in HALF_RATE else "F"
+    return valu_rate(m.group(1))
 
 
 def annotate(text):
@@ -64,7 +61,10 @@ def annotate(text):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    text, n = annotate(open(src).read())
+    try:
+        text, n = annotate(open(src).read())
+    except UnknownOpcode as e:
+        sys.exit(f"issue_prio: {src}: {e}")
     if n == 0:
         sys.exit("issue_prio: no VALU instruction found in " + src)
     open(dst, "w").write(text)

@@ -462,6 +462,7 @@ class Endpoint {
                         if (!kv.second.done && !kv.second.drained()) return false;
                     return true;
                 });
+                if (lost_unacked_) rc = LSP_ELOST;  // already forgotten ones (forget)
                 for (auto& kv : conns_)
                     if (kv.second.lost && kv.second.lost_while_closing) rc = LSP_ELOST;
             } else {
@@ -499,6 +500,7 @@ class Endpoint {
     Conn cli_;                   // client side: the one connection
     std::map<int, Conn> conns_;  // server side, by connID
     std::map<int, int> gone_;    // server side: connIDs whose end Read reported -> LSP_ELOST / LSP_ECLOSED
+    bool lost_unacked_ = false;  // server side: a forgotten conn was lost while closing with data unacked
     std::map<uint64_t, int> by_addr_;
     int next_id_ = 1;
 
@@ -530,12 +532,20 @@ class Endpoint {
     }
 
     // A server connection whose terminal event the caller has read: drop its
-    // buffers, remember only how it ended (for later write / close_conn).
+    // buffers, remember only how it ended (for later write / close_conn), and
+    // whether it was lost with messages unacked while closing (for Close).
+    // Only the last kGoneCap ended connIDs are remembered (ids only grow, so
+    // the smallest go first): a long-running server seeing many short client
+    // connections stays bounded, and a write to a long-forgotten id gets
+    // LSP_EINVAL instead of its old LSP_ELOST / LSP_ECLOSED.
+    static constexpr size_t kGoneCap = 1u << 16;
     void forget(int id, int rc) {
         auto it = conns_.find(id);
         if (it == conns_.end() || !it->second.done) return;
+        if (it->second.lost && it->second.lost_while_closing) lost_unacked_ = true;
         gone_[id] = rc;
         conns_.erase(it);
+        while (gone_.size() > kGoneCap) gone_.erase(gone_.begin());
     }
 
     // -- datagrams out (mu_ held) --

@@ -324,11 +324,19 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     mh::absorb_prefix(msg, len, &pre);
     // One device and adaptive chunks: nothing to balance, so one search (one
     // plan, full-size launches) instead of a chain of shrinking chunks.
-    if (ndev == 1 && chunk == 0 && getenv("MINEHIP_TEST_FAIL_WORKER") == nullptr)
+    // test hook of the dev build only (`make dev`, -DMH_DEV_HOOKS):
+    // MINEHIP_TEST_FAIL_WORKER=i makes worker i's first search fail with
+    // MH_EHIP, to exercise the hand-back path on a one-GPU box
+    int fail_worker = -1;
+#ifdef MH_DEV_HOOKS
+    if (const char* e = getenv("MINEHIP_TEST_FAIL_WORKER")) fail_worker = atoi(e);
+#endif
+    if (ndev == 1 && chunk == 0 && fail_worker < 0)
         return search_impl(devs[0], pre, lower, upper, out_hash, out_nonce);
     // One miner per listed device, fed by the server's scheduler (sched.hpp):
-    // chunks sized from each device's measured rate (~200 ms of work, >= 2^28
-    // nonces so the per-chunk plan + launch tail + sync stays well under 1%),
+    // chunks sized from each device's measured rate (the scheduler's default
+    // target_ns, 250 ms of work, include/minehip_server.h; >= 2^28 nonces so
+    // the per-chunk plan + launch tail + sync stays well under 1%),
     // capped at a fair share of what is left so the tail is spread over all
     // devices.  A device that fails hands its chunk back to the others.
     mh_sched_opts o;
@@ -338,7 +346,6 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     } else {
         o.init_chunk = 1ull << 32;
         o.min_chunk = 1ull << 28;
-        o.target_ns = 200000000ull;
     }
     mh::Scheduler sched(o);
     for (int i = 0; i < ndev; ++i) sched.add_miner(i);
@@ -355,10 +362,6 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
                    std::chrono::steady_clock::now().time_since_epoch())
             .count();
     };
-    // test hook: MINEHIP_TEST_FAIL_WORKER=i makes worker i's first search fail
-    // with MH_EHIP, to exercise the hand-back path on a one-GPU box
-    int fail_worker = -1;
-    if (const char* e = getenv("MINEHIP_TEST_FAIL_WORKER")) fail_worker = atoi(e);
     std::vector<std::thread> th;
     for (int i = 0; i < ndev; ++i) {
         th.emplace_back([&, i]() {
@@ -378,7 +381,7 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
                     continue;
                 }
                 uint64_t h, nn;
-                const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (MINEHIP_TEST_FAIL_WORKER)")
+                const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
                                                  : search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
                 if (r) {
                     const std::string e = g_err;

@@ -146,18 +146,24 @@ __global__ __launch_bounds__(kMergeThreads) void merge_partials(const Partial* _
 // host-side launchers
 // ---------------------------------------------------------------------------
 // fast_search<J, MODE> lives in a code object of its own, loaded once per
-// device and launched by its mangled name.  MINEHIP_DEV_CODE_OBJECT
-// (experiments only, tools/isa_variant.py) names a code object file to use
-// instead, e.g. the same kernels without the issue-priority pass; it is read
-// on every launch so tools/kbench.py can interleave variants in one process.
+// device and launched by its mangled name.  The product library knows only the
+// embedded code object.  The dev build (`make dev`, -DMH_DEV_HOOKS,
+// build/dev/libminehip.so; never shipped as the package's library) also
+// reads MINEHIP_DEV_CODE_OBJECT, a code object file to use instead (e.g. the
+// same kernels without the issue-priority pass, tools/isa_variant.py), on
+// every launch so that tools/kbench.py can interleave variants in one process.
 namespace {
 std::mutex g_mod_mu;
 std::map<std::pair<std::string, int>, hipModule_t> g_mods;                    // (file or "", dev)
 std::map<std::pair<hipModule_t, int>, hipFunction_t> g_funcs;                // (module, J + 16 * mode)
 
 hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f) {
+#ifdef MH_DEV_HOOKS
     const char* co = getenv("MINEHIP_DEV_CODE_OBJECT");
     const std::string path = (co && *co) ? co : "";
+#else
+    const std::string path;
+#endif
     std::lock_guard<std::mutex> g(g_mod_mu);
     auto it = g_mods.find({path, dev});
     if (it == g_mods.end()) {
@@ -205,12 +211,16 @@ hipError_t fast_module_init(int dev) {
 hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks,
                        hipStream_t s) {
     if (!fast_variant_exists(J, mode)) return hipErrorInvalidValue;
-    // MINEHIP_DEV_LDS (experiments only): reserve dynamic LDS per workgroup to
+#ifdef MH_DEV_HOOKS
+    // MINEHIP_DEV_LDS (dev build only): reserve dynamic LDS per workgroup to
     // cap occupancy, e.g. 54000 -> 3 workgroups (waves/SIMD) per CU.
     static const unsigned lds = [] {
         const char* e = getenv("MINEHIP_DEV_LDS");
         return e ? (unsigned)atoi(e) : 0u;
     }();
+#else
+    constexpr unsigned lds = 0;
+#endif
     hipFunction_t f;
     const hipError_t e = fast_function(dev, J, mode, &f);
     if (e != hipSuccess) return e;

@@ -3,12 +3,17 @@
 The library is built in-tree (``make`` at the repo root, or
 ``__graft_entry__.build()``) next to this file.  There is no fallback: if the
 shared object is missing, importing this module raises.
+
+MINEHIP_LIB names another build of the same ABI to load instead -- the dev
+build (``make dev``: build/dev/libminehip.so, with the experiment and test
+hooks) for tools/kbench.py A/Bs and the GPU tests that inject failures.
 """
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libminehip.so")
+PRODUCT_LIB_PATH = os.path.join(_HERE, "libminehip.so")
+LIB_PATH = os.environ.get("MINEHIP_LIB") or PRODUCT_LIB_PATH
 
 MH_OK = 0
 MH_EINVAL = -1

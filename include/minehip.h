@@ -77,7 +77,8 @@ int mh_search(int dev, const uint8_t *msg, size_t len, uint64_t lower, uint64_t 
  * listed device, merged on the host by the same lexicographic min
  * (associative, so bit-exact with mh_search).  No device-to-device traffic:
  * each chunk returns one 16-byte (hash, nonce).  chunk == 0: adaptive chunks
- * (~100 ms of each device's measured rate, capped at a fair share of what is
+ * (250 ms of each device's measured rate -- the scheduler's default
+ * target_ns, include/minehip_server.h -- capped at a fair share of what is
  * left); chunk > 0: fixed chunks of that many nonces.  A device that fails
  * hands its chunk back to the others; the call fails only if every device
  * fails (with the first failure's code). */

@@ -39,6 +39,23 @@ def golden_scan():
     return [conv(v) for v in d["small"]], [conv(v) for v in d["config1"]]
 
 
+DEV_LIB = os.path.join(ROOT, "build", "dev", "libminehip.so")
+
+
+def run_dev(code, timeout=120, **env):
+    """Run `code` in a child Python process whose minehip package loads the dev
+    build (build/dev/libminehip.so: the product sources plus the experiment and
+    test hooks, `make dev`), with extra environment `env`.  The product library
+    has no hooks (tests/test_abi.py::test_product_library_has_no_dev_hooks), so
+    a test that injects a failure runs here.  Returns the CompletedProcess."""
+    if not os.path.exists(DEV_LIB):
+        pytest.fail(f"{DEV_LIB} missing: build it with `make all` (or `make dev`)")
+    e = dict(os.environ, MINEHIP_LIB=DEV_LIB, **{k: str(v) for k, v in env.items()})
+    pre = f"import sys; sys.path[:0] = [{ROOT!r}, {PKG!r}]\n"
+    return subprocess.run([sys.executable, "-c", pre + code], env=e, capture_output=True, text=True,
+                          timeout=timeout)
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import minehip

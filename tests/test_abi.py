@@ -30,6 +30,21 @@ def test_exports_every_declared_symbol():
         assert hasattr(raw, s), s
 
 
+def test_product_library_has_no_dev_hooks():
+    """The experiment and test hooks (code-object override, LDS cap, injected worker failure)
+    exist only in the dev build (`make dev`), never in the package's library (VERDICT r02 #6)."""
+    hooks = (b"MINEHIP_DEV_CODE_OBJECT", b"MINEHIP_DEV_LDS", b"MINEHIP_TEST_FAIL_WORKER")
+    prod = open(_lib.PRODUCT_LIB_PATH, "rb").read()
+    assert not [h for h in hooks if h in prod]
+    from conftest import DEV_LIB
+    if os.path.exists(DEV_LIB):
+        dev = open(DEV_LIB, "rb").read()
+        assert all(h in dev for h in hooks)
+    # and the package loads the product library unless told otherwise
+    if not os.environ.get("MINEHIP_LIB"):
+        assert _lib.LIB_PATH == _lib.PRODUCT_LIB_PATH
+
+
 def test_abi_version_and_devices():
     assert minehip.lib.mh_abi_version() == 2
     assert minehip.device_count() >= 0

@@ -1,0 +1,87 @@
+"""CPU tests of bench.py's roofline line: `frac` is the
+algorithm's per-nonce work over the VALU issue peak and cannot exceed 1;
+SURVEY D4's pricing is reported beside it as `frac_survey_d4`; the dominant
+kernel's registers come from the embedded code object.  Host only: the plan
+(mh_plan) and the code-object metadata need no GPU."""
+import pytest
+
+import bench
+import minehip
+from minehip import codeobj
+
+CUS = 256
+
+
+def dominant_piece(cfg_name):
+    cfg = bench.CONFIGS[cfg_name]
+    lo, hi = bench.job_range(cfg, 1, 0, 1 if cfg["scaling"] == "weak" else 20)
+    fast = [p for p in minehip.plan(cfg["msg"], lo, hi) if p["kind"] == 0]
+    return max(fast, key=lambda p: p["count"] * p["nonce_slots"])
+
+
+def kstat(p, ns):
+    return {"name": f"mh::fast_search<{p['word']}, {p['mode']}>", "word": p["word"], "mode": p["mode"],
+            "launches": 1, "nonces": p["count"], "ns": int(ns), "ops": p["count"] * p["nonce_ops"],
+            "slots": p["count"] * p["nonce_slots"]}
+
+
+def fastest_possible_ns(p, sclk=bench.PEAK_SCLK_HZ):
+    """The shortest time the launch can take at the VALU issue limit: every SIMD quad-cycle
+    issues two wave64 instructions, except that a half-rate one never shares its quad-cycle
+    with another half-rate one -> >= max(H, N/2) quad-cycles per 64 nonces."""
+    n, h = p["nonce_ops"], p["nonce_slots"] - p["nonce_ops"]
+    quads = p["count"] / 64 * max(h, n / 2)
+    return quads * 4 / (CUS * 4 * sclk) * 1e9
+
+
+@pytest.mark.parametrize("cfg", ["2", "3a", "3b", "4"])
+def test_frac_is_a_fraction_at_the_issue_limit(cfg):
+    p = dominant_piece(cfg)
+    line = bench.roofline([kstat(p, fastest_possible_ns(p))], CUS, 1)
+    # at the fastest time the hardware allows, frac equals the mix bound, which is <= 1
+    assert line["frac"] <= 1.0
+    assert line["frac"] == pytest.approx(line["mix_bound_frac"], rel=2e-3)
+    assert line["frac_of_mix_bound"] == pytest.approx(1.0, rel=2e-3)
+    assert line["alg_instr_per_nonce"] == p["nonce_ops"]
+    # D4 prices a nonce at full compressions, so its ratio is larger (3b's exceeds 1)
+    assert line["frac_survey_d4"] > line["frac"]
+    if cfg == "3b":
+        assert line["frac_survey_d4"] > 1.0
+
+
+@pytest.mark.parametrize("cfg", ["2", "3a", "3b", "4"])
+def test_frac_from_measured_kernel_rates(cfg):
+    """The round-2 measured kernel rates (49.9 / 55.4 / 48.3 / 50.8 GH/s on
+    the dominant kernel or better) give fractions in (0, 1)."""
+    p = dominant_piece(cfg)
+    for ghs in (30.0, 50.0, 60.0):
+        line = bench.roofline([kstat(p, p["count"] / ghs)], CUS, 1)
+        assert 0.0 < line["frac"] < 1.0, (cfg, ghs, line["frac"])
+        assert line["frac"] == pytest.approx(ghs * 1e9 * p["nonce_ops"] / 1e12 / line["peak"], rel=1e-3)
+
+
+def test_frac_recomputes_from_a_kernel_trace():
+    """frac recomputed from a rocprofv3 kernel-trace average (profiles/
+    r02at_kernel_stats.csv: fast_search<4,0> 70.08 ms over 3,294,967,000 nonces) is
+    nonce_ops x nonces / avg / peak."""
+    p = dominant_piece("2")
+    assert (p["word"], p["mode"]) == (4, 0)
+    line = bench.roofline([kstat(p, 70_080_409.8)], CUS, 1)
+    want = p["nonce_ops"] * p["count"] / 0.0700804098 / 1e12 / (CUS * 128 * 2.4e9 / 1e12)
+    assert line["frac"] == pytest.approx(want, rel=1e-3)
+    assert line["frac"] < 0.75
+
+
+def test_resources_from_the_embedded_code_object():
+    res = codeobj.fast_kernel_resources()
+    want = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(j, 2) for j in (13, 14, 15)}
+    assert set(res) == want
+    for k, r in res.items():
+        assert r["scratch_bytes"] == 0 and r["vgpr_spills"] == 0, k
+        assert 32 <= r["vgpr"] <= 128 and r["agpr"] == 0, k
+        assert r["max_waves_per_simd"] >= 4, k
+    p = dominant_piece("2")
+    line = bench.roofline([kstat(p, 7e7)], CUS, 1, res)
+    assert line["resources"]["vgpr"] == res[(4, 0)]["vgpr"]
+    assert codeobj.max_waves_per_simd(69) == 7 and codeobj.max_waves_per_simd(64) == 8
+    assert codeobj.max_waves_per_simd(97) == 4 and codeobj.max_waves_per_simd(129) == 3

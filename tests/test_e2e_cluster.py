@@ -145,3 +145,56 @@ def test_cluster_gpu_with_killed_miner(gpu, tmp_path):
     h, n = gpu.search("cmu440", 0, max_nonce)
     assert out == f"Result {h} {n}", err[-2000:]
     assert "lost" in err and "requeued so far 0" not in err, err[-2000:]
+
+
+def _server(tmp, env=ENV):
+    port = free_udp_port()
+    serr = open(os.path.join(tmp, "server.err"), "w")
+    srv = subprocess.Popen([os.path.join(BIN, "minehip-server"), str(port)], stdout=subprocess.PIPE,
+                           stderr=serr, env=env, text=True)
+    assert srv.stdout.readline().strip() == f"Server listening on port {port}"
+    return srv, port
+
+
+def test_request_too_large_for_a_miner_frame_is_refused(tmp_path):
+    """a client Request that fits one LSP datagram can grow past one when the server
+    re-encodes it per miner chunk (Go's JSON escapes '<' as \\u003c: 6x).  The server refuses it up
+    front and closes the client, which then sees its connection end (the minehip-client prints
+    Disconnected), instead of the chunk write failing with LSP_ETOOBIG and the client waiting
+    forever.  A Request just under the limit is still served."""
+    from minehip import lsp
+    import minehip
+    srv, port = _server(str(tmp_path))
+    try:
+        miner, err = lsp.NewClient(f"127.0.0.1:{port}", lsp.NewParams(epoch_limit=5, epoch_millis=100))
+        assert err is None
+        assert miner.Write(minehip.marshal(minehip.NewJoin())) is None
+        time.sleep(0.3)
+        p = lsp.NewParams(epoch_limit=5, epoch_millis=100)
+        # a non-Go client writes '<' raw: 14,000 bytes of Data, ~19 KB as one datagram
+        big = b'{"Type":1,"Data":"' + b"<" * 14_000 + b'","Lower":0,"Upper":9}'
+        cl, err = lsp.NewClient(f"127.0.0.1:{port}", p)
+        assert err is None
+        assert cl.Write(big) is None
+        payload, err = cl.Read(timeout_ms=20_000)
+        assert payload is None and err is not None        # closed by the server, no Result
+        assert err.code in (lsp.LSP_ELOST, lsp.LSP_ECLOSED), err   # not a read timeout
+        assert "too large" in open(os.path.join(str(tmp_path), "server.err")).read()
+        cl.Close()
+        # 7,000 '<' re-encode to 42 KB + bounds: one datagram (base64 ~ 56 KB < 65,507 B): served
+        ok = b'{"Type":1,"Data":"' + b"<" * 7_000 + b'","Lower":0,"Upper":9}'
+        cl, err = lsp.NewClient(f"127.0.0.1:{port}", p)
+        assert cl.Write(ok) is None
+        req, err = miner.Read(timeout_ms=20_000)
+        assert err is None
+        m = minehip.unmarshal(req)
+        assert m.Type == minehip.Request and m.Data == b"<" * 7_000 and (m.Lower, m.Upper) == (0, 9)
+        h, n = oracle.search(m.Data, 0, 9, threads=1)
+        assert miner.Write(minehip.marshal(minehip.NewResult(h, n))) is None
+        res, err = cl.Read(timeout_ms=20_000)
+        assert err is None and minehip.unmarshal(res) == minehip.NewResult(h, n)
+        cl.Close()
+        miner.Close()
+    finally:
+        srv.kill()
+        srv.wait()

@@ -235,12 +235,24 @@ def test_profile_counters(gpu):
 
 def test_fast_kernels_run_from_the_embedded_module(gpu):
     """fast_search<J, MODE> runs from the code object embedded in libminehip.so (the issue-priority
-    build): pointing the dev hook at a missing file makes a fast search fail loudly
-    -- nothing falls back to another copy of the kernels -- and the embedded module serves the
-    next search again."""
+    build).  In the dev build (the same sources plus hooks, run in a child process),
+    pointing MINEHIP_DEV_CODE_OBJECT at a missing file makes a fast search fail loudly -- nothing
+    falls back to another copy of the kernels -- and the embedded module serves the next search
+    again.  The product library has no such hook (test_abi.py::test_product_library_has_no_dev_hooks)."""
+    from conftest import run_dev
     lo = 10 ** 9
-    with env(MINEHIP_DEV_CODE_OBJECT="/nonexistent/fast_search.hsaco"):
-        with pytest.raises(gpu.MinehipError) as e:
-            gpu.search(b"cmu440", lo, lo + (1 << 24) - 1)
-        assert e.value.code == gpu.MH_EHIP
-    assert gpu.search(b"cmu440", lo, lo + 199_999) == oracle.search(b"cmu440", lo, lo + 199_999, threads=4)
+    r = run_dev(f"""
+import os, minehip
+assert minehip.LIB_PATH.endswith("build/dev/libminehip.so"), minehip.LIB_PATH
+os.environ["MINEHIP_DEV_CODE_OBJECT"] = "/nonexistent/fast_search.hsaco"
+try:
+    minehip.search(b"cmu440", {lo}, {lo + (1 << 24) - 1})
+    raise SystemExit("fast search ran without its code object")
+except minehip.MinehipError as e:
+    assert e.code == minehip.MH_EHIP, e
+del os.environ["MINEHIP_DEV_CODE_OBJECT"]
+print(*minehip.search(b"cmu440", {lo}, {lo + 199_999}))
+""")
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = tuple(int(x) for x in r.stdout.split()[-2:])
+    assert got == oracle.search(b"cmu440", lo, lo + 199_999, threads=4)

@@ -70,16 +70,22 @@ def test_search_multi_adaptive_and_fixed(gpu):
 
 def test_search_multi_device_failure_hand_back(gpu):
     """A worker whose device fails hands its chunk back; the others finish
-    with the same answer.  If every worker fails, the call fails."""
-    import os
+    with the same answer.  If every worker fails, the call fails.  The
+    failure is injected by the dev build's MINEHIP_TEST_FAIL_WORKER hook, in a
+    child process (the product library has no hooks)."""
+    from conftest import run_dev
     hi = (1 << 31) - 1
     exp = gpu.search("cmu440", 0, hi)
-    os.environ["MINEHIP_TEST_FAIL_WORKER"] = "1"
-    try:
-        assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0, 0], chunk=1 << 27) == exp
-        os.environ["MINEHIP_TEST_FAIL_WORKER"] = "0"   # the only worker fails
-        with pytest.raises(gpu.MinehipError) as e:
-            gpu.search_multi("cmu440", 0, hi, devs=[0], chunk=1 << 27)
-        assert e.value.code == gpu.MH_EHIP and "injected" in str(e.value)
-    finally:
-        del os.environ["MINEHIP_TEST_FAIL_WORKER"]
+    r = run_dev(f"""
+import os, minehip
+os.environ["MINEHIP_TEST_FAIL_WORKER"] = "1"
+print(*minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0, 0], chunk=1 << 27))
+os.environ["MINEHIP_TEST_FAIL_WORKER"] = "0"   # the only worker fails
+try:
+    minehip.search_multi("cmu440", 0, {hi}, devs=[0], chunk=1 << 27)
+    raise SystemExit("search_multi succeeded with its only worker failing")
+except minehip.MinehipError as e:
+    assert e.code == minehip.MH_EHIP and "injected" in str(e), e
+""")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert tuple(int(x) for x in r.stdout.split()[-2:]) == exp

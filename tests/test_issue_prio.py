@@ -69,6 +69,37 @@ def test_classes():
     assert issue_prio.valu_class("\ts_add_u32 s0, s1, s2") is None
 
 
+def test_unknown_opcode_is_an_error():
+    # an opcode in neither table must not default to a class
+    with pytest.raises(issue_prio.UnknownOpcode):
+        issue_prio.valu_class("\tv_lshl_add_u32_e64 v1, v2, 3, v4")
+    with pytest.raises(issue_prio.UnknownOpcode):
+        issue_prio.annotate(ASM.replace("v_xor_b32_e32 v9, v7, v9", "v_new_op_b32 v9, v7, v9"))
+
+
+def test_unknown_opcode_fails_the_build_step(tmp_path):
+    src = tmp_path / "in.s"
+    src.write_text(ASM.replace("v_add_u32_e32 v6, v4, v6", "v_add_u32_sdwa v6, v4, v6"))
+    r = subprocess.run([sys.executable, os.path.join(PKG, "csrc", "issue_prio.py"), str(src),
+                        str(tmp_path / "out.s")], capture_output=True, text=True)
+    assert r.returncode != 0
+    assert "v_add_u32_sdwa" in r.stderr
+    assert not (tmp_path / "out.s").exists()
+
+
+def test_tables_are_disjoint_and_cover_the_real_build():
+    from valu_rates import FULL, HALF
+    assert not FULL & HALF
+    asm = os.path.join(os.path.dirname(PKG), "build", "fast_search.s")
+    if not os.path.exists(asm):
+        pytest.skip("build/fast_search.s not built (make all)")
+    ops = set(re.findall(r"^\s+(v_\w+)", open(asm).read(), flags=re.M))
+    assert ops and ops <= FULL | HALF, sorted(ops - (FULL | HALF))
+    # and the pass accepts the real compiler output as is
+    _, n = issue_prio.annotate(open(asm).read())
+    assert n > 10000
+
+
 def embedded_code_object():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     begin = ctypes.addressof(ctypes.c_char.in_dll(lib, "mh_fast_co_begin"))

@@ -383,6 +383,26 @@ def test_close_conn_and_server_close():
     b.Close()
 
 
+def test_server_close_reports_a_conn_lost_while_closing_after_read_reported_it():
+    """a connection lost during CloseConn with data still unacked makes Server.Close
+    return LSP_ELOST -- also when Read has already reported the loss and freed the connection."""
+    p = fast(limit=3, millis=50)
+    srv, _ = lsp.NewServer(0, p)
+    peer = RawPeer()
+    peer.addr = ("127.0.0.1", srv.port)
+    peer.send(lsp.MsgConnect)
+    m, _ = peer.recv(2)
+    cid = m["ConnID"]
+    peer.close()                                  # the client goes silent: nothing is ever acked
+    assert srv.Write(cid, b"never acked") is None
+    assert srv.CloseConn(cid) is None
+    c, got, err = srv.Read(3000)                  # lost while closing, reported, then forgotten
+    assert (c, got, err.code) == (cid, None, lsp.LSP_ELOST)
+    assert srv.Write(cid, b"x").code == lsp.LSP_ELOST
+    err = srv.Close()
+    assert err is not None and err.code == lsp.LSP_ELOST
+
+
 def test_client_close_waits_for_acks_under_loss():
     # lsp4_test.go ClientClose: Close blocks until pending messages are acked,
     # here with the network dropping everything at first.

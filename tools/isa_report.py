@@ -13,13 +13,11 @@ import re
 import sys
 from collections import Counter
 
-# measured on MI355X (tools/valu_ops.hip): ~63 lanes/clk/CU instead of ~120
-HALF_RATE = {
-    "v_alignbit_b32", "v_alignbyte_b32", "v_add3_u32", "v_xad_u32", "v_bfi_b32", "v_lshl_or_b32",
-    "v_lshl_add_u32", "v_and_or_b32", "v_or3_b32", "v_perm_b32", "v_cndmask_b32_e64", "v_mad_u32_u24",
-    "v_lshrrev_b64", "v_lshlrev_b64", "v_mov_b64", "v_lshlrev_b32_e64", "v_lshrrev_b32_e64",
-    "v_mad_u64_u32", "v_pk_add_u16",
-}
+import os  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "bitcoin-miner_amd", "csrc"))
+from valu_rates import HALF as HALF_RATE  # noqa: E402  (one table with the issue-priority pass)
 
 
 def kernels(text):

@@ -1,5 +1,5 @@
 """Build gfx950 code objects of search_kernels.hip with hand-edited ISA, for
-A/B runs through the library's MINEHIP_DEV_CODE_OBJECT hook (experiments
+A/B runs through the dev build's MINEHIP_DEV_CODE_OBJECT hook (`make dev`; experiments
 only).
 
   python tools/isa_variant.py base e64      # -> build/isa/<variant>.hsaco (from fast_search.hip)
@@ -77,8 +77,8 @@ def in_fast(text):
 
 # source-level variants: the kernel source compiled with extra defines
 DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
-    "sync1": (["-DMH_SYNC=1"], False),    # s_barrier before every nonce: the 4 waves of a workgroup in step
-    "sync10": (["-DMH_SYNC=10"], False),  # s_barrier before every group of 10 nonces
+    # (the s_barrier variants sync1/sync10 of round 2, -4%, profiles/r02k_kbench_sync.json, were removed
+    # from the kernel source in round 3)
     "prio_w8": (["-DMH_MIN_WAVES=8"], True),   # <= 64 VGPRs: 8 waves/SIMD
     "prio_w6": (["-DMH_MIN_WAVES=6"], True),
     "prio_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], True),

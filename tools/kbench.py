@@ -4,6 +4,10 @@ configurations given as env settings inside ONE process.
 
   python tools/kbench.py --msg cmu440 --lo 1000000000 --count 2147483648 \
       --var base: --var lds3:MINEHIP_DEV_LDS=54000 --rounds 3
+
+A --var that sets a MINEHIP_DEV_* hook needs the dev build of the library
+(`make dev`); kbench then loads build/dev/libminehip.so for every variant, so
+the A/B compares like with like.  The product library has no hooks.
 """
 import argparse
 import json
@@ -18,6 +22,8 @@ if len(sys.argv) > 2 and sys.argv[1] == "--pkg":
     del sys.argv[1:3]
 else:
     sys.path[:0] = [ROOT, os.path.join(ROOT, "bitcoin-miner_amd")]
+if any("MINEHIP_DEV_" in a for a in sys.argv) and not os.environ.get("MINEHIP_LIB"):
+    os.environ["MINEHIP_LIB"] = os.path.join(ROOT, "build", "dev", "libminehip.so")
 import minehip  # noqa: E402
 
 
