@@ -285,10 +285,18 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
             }
             // New wave best (rare): a uniform branch, so H1 and the
             // lexicographic compare cost nothing on the common path.
-            const uint64_t cm = __builtin_amdgcn_ballot_w64(h0 <= wbh0) & valid_mask;
+            uint64_t cm = __builtin_amdgcn_ballot_w64(h0 <= wbh0) & valid_mask;
             if (__builtin_expect(cm != 0ull, 0)) {
                 const uint32_t h1 = st[1] + a63;
                 const uint32_t q = g * 10u + i;
+                // Many candidates (the first nonce of a run makes every lane one): keep only
+                // the lanes holding their smallest H0, found by a DPP wave-min, instead of a
+                // 64-step scalar scan (~1,000 serial SALU / readlane instructions per run).
+                if (__builtin_popcountll(cm) > 4) {
+                    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                    const uint32_t mh = wave_min_u32(((cm >> lane) & 1ull) ? h0 : 0xFFFFFFFFu);
+                    cm &= __builtin_amdgcn_ballot_w64(h0 == mh);
+                }
                 uint64_t m = cm;
                 do {
                     const uint32_t l = (uint32_t)__builtin_ctzll(m);

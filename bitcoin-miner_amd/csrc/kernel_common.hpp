@@ -35,6 +35,19 @@ __device__ __forceinline__ void wave_step(uint64_t& h, uint64_t& n) {
     }
 }
 
+// Wave-wide minimum of a u32 (every lane active): DPP butterfly within each
+// 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror),
+// then the four rows' minima through readlane and scalar mins.  Wave-uniform.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    return min(min(a, b), min(c, d));
+}
+
 // Workgroup lexicographic min; the result is valid in thread 0.
 // Wave level: DPP quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror,
 // row_mirror (each step joins two groups whose lanes already agree, so after

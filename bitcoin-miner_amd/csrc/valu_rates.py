@@ -47,6 +47,8 @@ HALF_ASSUMED = frozenset({
     "v_cmp_gt_u64_e32", "v_cmp_ge_u64_e32",
     "v_cmp_eq_u64_e64", "v_cmp_ne_u64_e64", "v_cmp_lt_u64_e64", "v_cmp_le_u64_e64",
     "v_cmp_gt_u64_e64", "v_cmp_ge_u64_e64",
+    "v_min_u32_dpp", "v_min3_u32", "v_mbcnt_lo_u32_b32", "v_mbcnt_hi_u32_b32",
+    # ^ the candidate wave-min (kernel_common.hpp wave_min_u32), in the rare new-best branch
 })
 FULL = FULL_MEASURED | FULL_ASSUMED
 HALF = HALF_MEASURED | HALF_ASSUMED

@@ -198,3 +198,50 @@ def test_request_too_large_for_a_miner_frame_is_refused(tmp_path):
     finally:
         srv.kill()
         srv.wait()
+
+
+# ---- BASELINE configs[4] at its stated size -----------------------------
+CFG5_HI = (1 << 42) - 1
+_cfg5 = {}
+
+
+def _cfg5_direct(gpu):
+    """One direct mh_search of configs[4]'s range (~90 s), shared by the tests below."""
+    if "direct" not in _cfg5:
+        _cfg5["direct"] = gpu.search(b"cmu440", 0, CFG5_HI)
+    return _cfg5["direct"]
+
+
+def _cfg5_checks(gpu, got):
+    """configs[4]'s answer against everything that pins it without a CPU scan of 2^42 nonces."""
+    from conftest import load_golden
+    msg = b"cmu440"
+    assert gpu.Hash(msg, got[1]) == got[0]                        # re-hashed by the generic kernel
+    cfg4 = load_golden("fullsize_cfg4.json")                      # [0, 2^40-1] is a prefix of the range
+    assert got <= tuple(cfg4["result"])
+    s = load_golden("fullsize_cfg4s.json")                        # 100 OpenSSL-scanned 2^24 chunks
+    assert all(got <= (h, n) for lo, hi, h, n in s["samples"] if hi <= CFG5_HI)
+    c = load_golden("fullsize_cfg5c.json")                        # the answer's 2^32 chunk, SHA-NI scan
+    assert c["lo"] <= got[1] <= c["hi"]
+    assert got == tuple(c["result"])                              # the CPU-verified minimum of its chunk
+
+
+@pytest.mark.gpu
+def test_config5_direct_search(gpu):
+    """BASELINE configs[4]'s range, "cmu440" over [0, 2^42-1], searched directly on one GPU."""
+    _cfg5_checks(gpu, _cfg5_direct(gpu))
+
+
+@pytest.mark.gpu
+def test_config5_over_lsp_eight_gpu_miners_one_killed(gpu, tmp_path):
+    """BASELINE configs[4] at its stated size: server + 8 GPU miner processes (configs[4]'s
+    one-per-GPU layout; all on this box's GPU) + client over LSP/UDP, "cmu440" over
+    [0, 2^42-1], one miner SIGKILLed 5 s in.  The client's Result equals the direct search,
+    re-hashes, and is pinned by the fixtures (_cfg5_checks)."""
+    out, err = run_cluster([gpu_miner()] * 8, "cmu440", CFG5_HI, chunk=None, timeout=480,
+                           kill_after=(7, 5.0), tmp=str(tmp_path))
+    assert out.startswith("Result "), err[-2000:]
+    got = tuple(int(x) for x in out.split()[1:3])
+    _cfg5_checks(gpu, got)
+    assert got == _cfg5_direct(gpu)
+    assert "lost" in err and "requeued so far 0" not in err, err[-2000:]

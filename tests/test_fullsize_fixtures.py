@@ -22,6 +22,8 @@ CFGS.update({k: ((b"cmu440-" * 10)[:n], (1 << 32) - 1) for k, n in LAYOUTS.items
 CFGS.update({"pre3": ((b"cmu440-" * 10)[:62], 10 ** 13 + (1 << 32) - 1, 10 ** 13),
              "pre4": ((b"cmu440-" * 10)[:62], 10 ** 17 + (1 << 32) - 1, 10 ** 17),
              "top": (b"cmu440", (1 << 64) - 1, (1 << 64) - (1 << 32))})
+# BASELINE configs[4]'s answer chunk, [1017 * 2^32, 1018 * 2^32 - 1] in 2^28 chunks (gen_cfg5c.py, SHA-NI)
+CFGS["cfg5c"] = (b"cmu440", (1018 << 32) - 1, 1017 << 32)
 
 
 def _cfg(name):
@@ -49,7 +51,7 @@ def test_fixture_chunk_vs_oracle(name):
     d = load_golden(f"fullsize_{name}.json")
     msg, lo, _ = _cfg(name)
     size = 1 << d["chunk_bits"]
-    i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000}.get(name, 255)  # cfg*: d = 10, 11, 11 chunks; the rest: last
+    i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000, "cfg5c": 15}.get(name, 255)  # cfg*: d = 10, 11, 11; the rest: last
     got = oracle.search(msg, lo + i * size, lo + (i + 1) * size - 1, threads=os.cpu_count() or 1)
     assert got == tuple(d["chunks"][i])
 

@@ -24,6 +24,9 @@ reproduce every one of them:
   cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
   cfg4   "cmu440" [0, 2^40-1]: configs[3] whole, its 256 2^32-chunk minima
          (tests/golden/gen_cfg4.py: SHA-NI scan, checked against OpenSSL)
+  cfg5c  "cmu440" [1017 * 2^32, 1018 * 2^32 - 1]: the 2^32 chunk of configs[4] that holds its
+         answer, in 2^28 chunks (tests/golden/gen_cfg5c.py: SHA-NI scan, checked against OpenSSL);
+         configs[4] itself runs in test_e2e_cluster.py (direct and over LSP with 8 miners)
 
 Reference semantics: bitcoin/hash.go:13-17 and the scan spec of SURVEY.md
 §8(a) A2 (reference stub bitcoin/miner/miner.go:33).
@@ -38,7 +41,7 @@ from test_gpu_parity import env
 pytestmark = pytest.mark.gpu
 
 CFGS = ("cfg2", "cfg3a", "cfg3b", "two13", "two14", "two15", "pre0", "pre2", "pre3", "pre4", "top",
-        "one1", "one5", "one7", "one8", "one10", "one12")
+        "one1", "one5", "one7", "one8", "one10", "one12", "cfg5c")
 
 
 def fixture(name):

@@ -91,6 +91,22 @@ OP_KERNEL(k_bitop3_lit, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8")
 OP_KERNEL(k_lshlrev_e64, "v_lshlrev_b32_e64 %0, 7, %0")
 OP_KERNEL(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %2")
 OP_KERNEL(k_sdwa_xor, "v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD")
+// round 3: the opcodes valu_rates.py had classed by encoding only (ASSUMED)
+OP_KERNEL(k_min_dpp, "v_min_u32_dpp %0, %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+OP_KERNEL(k_mov_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+OP_KERNEL(k_min3, "v_min3_u32 %0, %0, %1, %2")
+OP_KERNEL(k_min_e32, "v_min_u32_e32 %0, %0, %1")
+OP_KERNEL(k_and_e32, "v_and_b32_e32 %0, %0, %1")
+OP_KERNEL(k_or_e32, "v_or_b32_e32 %0, %0, %1")
+OP_KERNEL(k_lshl_e32, "v_lshlrev_b32_e32 %0, %1, %0")
+OP_KERNEL(k_not_e32, "v_not_b32_e32 %0, %0")
+OP_KERNEL(k_sub_e64, "v_sub_u32_e64 %0, %0, %1")
+OP_KERNEL(k_cnd_e32, "v_cndmask_b32_e32 %0, %1, %0, vcc")
+OP_KERNEL(k_cmp_e32, "v_cmp_lt_u32_e32 vcc, %0, %1")
+OP_KERNEL(k_mul_lo, "v_mul_lo_u32 %0, %0, %1")
+OP_KERNEL(k_mul_hi, "v_mul_hi_u32 %0, %0, %1")
+OP_KERNEL(k_add_lshl, "v_add_lshl_u32 %0, %0, %1, 3")
+OP_KERNEL(k_lshr_e64, "v_lshrrev_b32_e64 %0, 7, %0")
 
 typedef void (*kfn)(uint32_t*, uint32_t, uint64_t*);
 
@@ -118,7 +134,12 @@ int main() {
               {"v_and_or_b32", k_and_or}, {"v_lshl_add_u32", k_lshl_add}, {"v_pk_add_u16", k_pk_add_u16},
               {"v_sub_u32_e32", k_sub_e32}, {"v_cndmask_b32_e64", k_cndmask}, {"v_add_u32_e32+lit", k_add_lit},
               {"v_bitop3_b32(maj)", k_bitop3_lit}, {"v_lshlrev_b32_e64", k_lshlrev_e64},
-              {"v_mad_u32_u24", k_mad_u24}, {"v_xor_b32_sdwa(w1)", k_sdwa_xor}};
+              {"v_mad_u32_u24", k_mad_u24}, {"v_xor_b32_sdwa(w1)", k_sdwa_xor},
+              {"v_min_u32_dpp", k_min_dpp}, {"v_mov_b32_dpp", k_mov_dpp}, {"v_min3_u32", k_min3},
+              {"v_min_u32_e32", k_min_e32}, {"v_and_b32_e32", k_and_e32}, {"v_or_b32_e32", k_or_e32},
+              {"v_lshlrev_b32_e32", k_lshl_e32}, {"v_not_b32_e32", k_not_e32}, {"v_sub_u32_e64", k_sub_e64},
+              {"v_cndmask_b32_e32", k_cnd_e32}, {"v_cmp_lt_u32_e32", k_cmp_e32}, {"v_mul_lo_u32", k_mul_lo},
+              {"v_mul_hi_u32", k_mul_hi}, {"v_add_lshl_u32", k_add_lshl}, {"v_lshrrev_b32_e64", k_lshr_e64}};
     printf("{\"cus\": %d, \"ops\": {", cus);
     const int nk = sizeof ks / sizeof ks[0];
     for (int w = 0; w < 2; ++w) {
