@@ -79,7 +79,9 @@ struct DevCtx {
     std::mutex mu;
     int dev = -1;
     bool ready = false;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;              // every search's merge and copy; pieces with streams = 1
+    hipStream_t s_hi = nullptr, s_lo = nullptr;  // streams = 2: coarse / fine pieces (priorities)
+    hipEvent_t ev_join[3] = {nullptr, nullptr, nullptr};
     Partial* d_partials = nullptr;
     Partial* d_best = nullptr;
     Partial* h_best = nullptr;  // pinned
@@ -130,6 +132,14 @@ int init_locked(DevCtx* c, int dev) {
     // each resource only once: a call after a failed init (e.g. the code object
     // did not load) resumes where that one stopped instead of allocating again
     if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!c->s_hi || !c->s_lo) {
+        int least = 0, greatest = 0;
+        MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        if (!c->s_hi) MH_HIP(hipStreamCreateWithPriority(&c->s_hi, hipStreamNonBlocking, greatest));
+        if (!c->s_lo) MH_HIP(hipStreamCreateWithPriority(&c->s_lo, hipStreamNonBlocking, least));
+    }
+    for (auto& e : c->ev_join)
+        if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!c->d_partials) MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
     if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
     if (!c->h_best) MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
@@ -159,17 +169,34 @@ int harvest_locked(DevCtx* c) {
     return MH_OK;
 }
 
-// Fold the pending partials into the running minimum.
-int flush_partials(DevCtx* c) {
-    if (c->poff) MH_HIP(mh::launch_merge(c->d_partials, c->poff, c->d_best, c->stream));
+// Fold the pending partials into the running minimum.  With two piece
+// streams the merge (on the main stream) first waits for both, and both wait
+// for the merge before any later piece reuses the partials buffer.
+int flush_partials(DevCtx* c, bool split) {
+    if (!c->poff) return MH_OK;
+    if (split) {
+        MH_HIP(hipEventRecord(c->ev_join[0], c->s_hi));
+        MH_HIP(hipEventRecord(c->ev_join[1], c->s_lo));
+        MH_HIP(hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
+        MH_HIP(hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
+    }
+    MH_HIP(mh::launch_merge(c->d_partials, c->poff, c->d_best, c->stream));
     c->poff = 0;
+    if (split) {
+        MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
+        MH_HIP(hipStreamWaitEvent(c->s_hi, c->ev_join[2], 0));
+        MH_HIP(hipStreamWaitEvent(c->s_lo, c->ev_join[2], 0));
+    }
     return MH_OK;
 }
 
 // Enqueue one piece on the context's stream.  Its workgroups write their
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
-int enqueue_piece(DevCtx* c, const mh::Piece& p) {
+int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
+    const bool split = opt.streams == 2;
+    // streams = 2: coarse pieces (the full L) on the high-priority stream, the rest on the low one
+    hipStream_t s = !split ? c->stream : (p.kind == 0 && p.L == opt.lower_digits) ? c->s_hi : c->s_lo;
     uint32_t blocks;
     if (p.kind == 0) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
@@ -184,7 +211,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
     }
     if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
     if (c->poff + blocks > mh::kMaxBlocksPerLaunch) {
-        const int rc = flush_partials(c);
+        const int rc = flush_partials(c, split);
         if (rc) return rc;
     }
     Partial* out = c->d_partials + c->poff;
@@ -192,19 +219,21 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
+            MH_HIP(hipStreamSynchronize(c->s_hi));
+            MH_HIP(hipStreamSynchronize(c->s_lo));
             int rc = harvest_locked(c);
             if (rc) return rc;
         }
         tm = &c->pool[(size_t)c->used++];
         tm->kind = p.kind;
         tm->var = p.J + 16 * p.mode;
-        MH_HIP(hipEventRecord(tm->start, c->stream));
+        MH_HIP(hipEventRecord(tm->start, s));
     }
     if (p.kind == 0)
-        MH_HIP(mh::launch_fast(c->dev, p.J, p.mode, p.fa, out, blocks, c->stream));
+        MH_HIP(mh::launch_fast(c->dev, p.J, p.mode, p.fa, out, blocks, s));
     else
-        MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, c->stream));
-    if (tm) MH_HIP(hipEventRecord(tm->stop, c->stream));
+        MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, s));
+    if (tm) MH_HIP(hipEventRecord(tm->stop, s));
     c->poff += blocks;
     if (c->prof) {
         if (p.kind == 0) {
@@ -231,6 +260,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p) {
 //   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^34)
 //   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
 //   MINEHIP_MAX_BLOCKS     workgroups per launch (1..kMaxBlocksPerLaunch)
+//   MINEHIP_STREAMS        1: one stream; 2: coarse / fine pieces on high / low priority streams
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -247,6 +277,10 @@ mh::PlanOpts plan_opts() {
         const unsigned long long v = strtoull(e, nullptr, 10);
         if (v >= 1 && v <= mh::kMaxBlocksPerLaunch) o.max_blocks = (uint32_t)v;
     }
+    if (const char* e = getenv("MINEHIP_STREAMS")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2) o.streams = v;
+    }
     return o;
 }
 
@@ -260,14 +294,22 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     MH_HIP(hipSetDevice(dev));
     MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
     const mh::PlanOpts opt = plan_opts();
+    const bool split = opt.streams == 2;
+    if (split) {  // both piece streams start after the reset (and after the previous search)
+        MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
+        MH_HIP(hipStreamWaitEvent(c->s_hi, c->ev_join[2], 0));
+        MH_HIP(hipStreamWaitEvent(c->s_lo, c->ev_join[2], 0));
+    }
     int err = MH_OK;
     c->poff = 0;
     mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
-        err = enqueue_piece(c, p);
+        err = enqueue_piece(c, p, opt);
         return err == MH_OK;
     });
-    if (!err) err = flush_partials(c);
+    if (!err) err = flush_partials(c, split);
     if (err) {
+        (void)hipStreamSynchronize(c->s_hi);
+        (void)hipStreamSynchronize(c->s_lo);
         (void)hipStreamSynchronize(c->stream);
         return err;
     }

@@ -59,6 +59,11 @@ struct PlanOpts {
     uint64_t max_nonces_per_launch = 1ull << 34; // one launch <= ~0.35 s (one tail block) / ~0.6 s (two)
     uint32_t max_blocks = 1u << 17;              // workgroups per launch (<= kMaxBlocksPerLaunch; +0.1% over 2^16)
     uint64_t generic_below = 1u << 20;           // a bucket this small goes to the generic kernel whole
+    // Execution (minehip.cpp, not the plan itself): 1 = every piece on one stream in nonce
+    // order; 2 = the pieces at the full L (coarse: 1,000-nonce lanes) on a high-priority
+    // stream, the others (shorter lanes, generic edges) on a low-priority one, so that the
+    // short workgroups back-fill the coarse launch's tail instead of each launch draining alone.
+    int streams = 1;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

@@ -92,7 +92,9 @@ def test_plan_knobs_full_size(gpu):
     msg, _, _, bits, _, chunks = fixture("cfg2")
     exp = min(chunks[:(1 << 32) >> bits])
     for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1 << 18),
-               dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0)):
+               dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0),
+               dict(MINEHIP_STREAMS=2), dict(MINEHIP_STREAMS=2, MINEHIP_LAUNCH_NONCES=1 << 30,
+                                             MINEHIP_MAX_BLOCKS=1 << 12)):
         with env(**kv):
             assert gpu.search(msg, 0, (1 << 32) - 1) == exp, kv
 

@@ -169,13 +169,15 @@ def test_plan_invariance_small(gpu):
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 2, 3, 4, 5):
             for gb in (0, 1 << 20):
-                with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
-                         MINEHIP_GENERIC_BELOW=gb):
-                    assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb)
-        # tiny grids: many launches per bucket and many partial-buffer flushes
+                for st in (1, 2):
+                    with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
+                             MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st):
+                        assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st)
+        # tiny grids: many launches per bucket and many partial-buffer flushes (on both streams)
         for mb in (1, 3, 1000):
-            with env(MINEHIP_MAX_BLOCKS=mb, MINEHIP_MIN_LANES=1):
-                assert gpu.search(m, lo, hi) == exp, (m[:8], mb)
+            for st in (1, 2):
+                with env(MINEHIP_MAX_BLOCKS=mb, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st):
+                    assert gpu.search(m, lo, hi) == exp, (m[:8], mb, st)
 
 
 @pytest.mark.parametrize("msg,bits", [(b"cmu440", 32), (b"a" * 100, 34), (b"x" * 60, 34)])
