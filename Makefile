@@ -48,7 +48,7 @@ $(DEVLIB): $(SRCS) $(HDRS) $(FAST_O)
 $(FAST_S): $(CSRC)/fast_search.hip $(FAST_HDRS)
 	mkdir -p $(BUILD)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $(FASTFLAGS) --cuda-device-only -S -o $@ $<
-$(FAST_PS): $(FAST_S) $(CSRC)/issue_prio.py
+$(FAST_PS): $(FAST_S) $(CSRC)/issue_prio.py $(CSRC)/valu_rates.py
 	python3 $(CSRC)/issue_prio.py $< $@
 $(FAST_CO): $(FAST_PS)
 	$(LLVM)/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c -o $(BUILD)/fast_search_prio.o $<

@@ -228,10 +228,11 @@ def cpu_baseline(msg, threads):
 
 
 def largest_piece(msg, lo, hi, var):
-    """The largest launch of fast_search<word, mode> in the plan of [lo, hi]."""
+    """The largest launch of fast_search<word, mode> with var's lane length in the plan of [lo, hi]."""
     import minehip
     ps = [p for p in minehip.plan(msg, lo, hi)
-          if p["kind"] == 0 and p["word"] == var["word"] and p["mode"] == var["mode"]]
+          if p["kind"] == 0 and p["word"] == var["word"] and p["mode"] == var["mode"]
+          and p["lo_digits"] == var.get("lo_digits", p["lo_digits"])]
     return max(ps, key=lambda p: p["count"]) if ps else None
 
 
@@ -347,11 +348,12 @@ def die(msg, code=2):
 
 
 def kernel_totals(per_dev_kstats):
-    """Sum the per-variant HIP-event stats over devices; largest time first."""
+    """Sum the per-(variant, lane length) HIP-event stats over devices; largest time first."""
     tot = {}
     for ks in per_dev_kstats:
         for k in ks:
-            t = tot.setdefault(k["name"], dict(k, launches=0, nonces=0, ns=0, ops=0, slots=0))
+            t = tot.setdefault((k["name"], k.get("lo_digits")),
+                               dict(k, launches=0, nonces=0, ns=0, ops=0, slots=0))
             for f in ("launches", "nonces", "ns", "ops", "slots"):
                 t[f] += k[f]
     return sorted(tot.values(), key=lambda k: -k["ns"])
@@ -409,6 +411,7 @@ def roofline(kst, cus, n_devices, resources=None):
                                "a nonce at full compressions, the kernel hoists what a lane's nonces "
                                "share, so this ratio credits the hoisting and can exceed 1",
         "kernel": dom["name"],
+        "lo_digits": dom.get("lo_digits"),     # the launches' lane length (10^L nonces per lane)
         "tail_blocks": blocks,
         "launches": dom["launches"],
         "devices": n_devices,
@@ -425,7 +428,8 @@ def roofline(kst, cus, n_devices, resources=None):
                                                "libminehip.so (minehip/codeobj.py)")
     if len(kst) > 1:
         s = kst[1]
-        line["second_kernel"] = {"kernel": s["name"], "ms": round(s["ns"] / 1e6, 3),
+        line["second_kernel"] = {"kernel": s["name"], "lo_digits": s.get("lo_digits"),
+                                 "ms": round(s["ns"] / 1e6, 3),
                                  "kernel_ghs": round(s["nonces"] / (s["ns"] * 1e-9) / 1e9, 4),
                                  "alg_instr_per_nonce": round(s["ops"] / max(1, s["nonces"]), 1),
                                  "frac": round(s["ops"] / (s["ns"] * 1e-9) / 1e12 / peak, 4)}
@@ -550,6 +554,11 @@ def main():
     kst = kernel_totals([p["kstats"] for p in per_dev])
     from minehip import codeobj
     roof = roofline(kst, cus, len(per_dev), codeobj.fast_kernel_resources())
+    # the whole timed region on the same basis: every fast piece's nonces x nonce_ops over the
+    # max-over-ranks wall time and all N GPUs' peak -- tails, generic edge launches, launch gaps,
+    # the host merge and concurrent streams included (generic nonces, < 0.1%, not credited)
+    all_ops = sum(p["prof"]["fast_ops"] for p in per_dev)
+    roof["search_frac"] = round(all_ops / t_max / 1e12 / (n_gpus * roof["peak"]), 4)
     # algorithmic bytes of the dominant launch: one 16-byte (hash, nonce) partial per 256-lane workgroup
     job_lo, job_hi = job_range(cfg, n_gpus, 0, 1 if cfg["scaling"] == "weak" else steps)
     my_lo, my_hi = (rank_range(cfg, rank, world, 0, steps) if launched else (job_lo, job_hi))

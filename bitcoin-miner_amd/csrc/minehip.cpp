@@ -66,14 +66,15 @@ constexpr int kEventPairs = 512;             // profiled launches buffered befor
 struct Timed {
     hipEvent_t start = nullptr, stop = nullptr;
     int kind;  // 0 fast, 1 generic
-    int var;   // fast: kernel variant index (J + 16 * mode)
+    int var;   // fast: kernel variant and lane length, var_index(J, mode, L)
 };
 
 // per fast_search<J, MODE> variant: launches, nonces, ns, algorithmic instructions
 struct VarStat {
     uint64_t launches = 0, nonces = 0, ns = 0, ops = 0, slots = 0;
 };
-constexpr int kVariants = 48;  // J < 16, mode < 3
+constexpr int kVariants = 16 * 3 * 5;  // J < 16, mode < 3, L = 1..5
+inline int var_index(int J, int mode, int L) { return J + 16 * mode + 48 * (L - 1); }
 
 struct DevCtx {
     std::mutex mu;
@@ -226,7 +227,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
         }
         tm = &c->pool[(size_t)c->used++];
         tm->kind = p.kind;
-        tm->var = p.J + 16 * p.mode;
+        tm->var = p.kind == 0 ? var_index(p.J, p.mode, p.L) : 0;
         MH_HIP(hipEventRecord(tm->start, s));
     }
     if (p.kind == 0)
@@ -241,7 +242,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
             c->cnt[1] += p.count;
             c->cnt[3] += p.count * (uint64_t)p.ops;
             c->cnt[6] += p.count * (uint64_t)p.slots;
-            VarStat& v = c->var[p.J + 16 * p.mode];
+            VarStat& v = c->var[var_index(p.J, p.mode, p.L)];
             v.launches += 1;
             v.nonces += p.count;
             v.ops += p.count * (uint64_t)p.ops;
@@ -260,7 +261,10 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
 //   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^34)
 //   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
 //   MINEHIP_MAX_BLOCKS     workgroups per launch (1..kMaxBlocksPerLaunch)
-//   MINEHIP_STREAMS        1: one stream; 2: coarse / fine pieces on high / low priority streams
+//   MINEHIP_STREAMS        1: one stream; 2: coarse / fine pieces on high / low priority
+//                          streams (default 2)
+//   MINEHIP_FINE_TAIL      nonces at the end of each full-L bucket planned at L - 1 (default
+//                          2^28; 0: none)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -281,6 +285,7 @@ mh::PlanOpts plan_opts() {
         const int v = atoi(e);
         if (v == 1 || v == 2) o.streams = v;
     }
+    if (const char* e = getenv("MINEHIP_FINE_TAIL")) o.fine_tail = strtoull(e, nullptr, 10);
     return o;
 }
 
@@ -537,7 +542,9 @@ int mh_profile_kernels(int dev, mh_kernel_stat* out, int cap) {
         if (!v.launches) continue;
         if (n < cap) {
             out[n].word = i % 16;
-            out[n].mode = i / 16;
+            out[n].mode = (i / 16) % 3;
+            out[n].lo_digits = i / 48 + 1;
+            out[n].reserved = 0;
             out[n].launches = v.launches;
             out[n].nonces = v.nonces;
             out[n].ns = v.ns;

@@ -294,30 +294,48 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const unsigned __int128 fast_end = U1p * R;  // exclusive, may be 2^64
         if (A < fast_first && !emit_generic(A, fast_first - 1u, d)) return;
         if (!flush_generic()) return;
-        const uint64_t max_runs =
-            std::max<uint64_t>(1u, std::min<uint64_t>(max_gen,
-                                                      opt.max_nonces_per_launch / (uint64_t)R));
-        for (unsigned __int128 u = U0; u < U1p;) {
-            const unsigned __int128 left = U1p - u;
-            const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
-            Piece p;
-            memset(&p, 0, sizeof p);
-            p.first = (uint64_t)(u * R);
-            p.count = (uint64_t)((unsigned __int128)runs * R);
-            p.kind = 0;
-            p.digits = d;
-            p.L = L;
-            p.J = J;
-            p.mode = mode;
-            p.blocks = nb;
-            p.fa = fa;
-            { const NonceCost nc = nonce_cost(J, mode); p.ops = nc.ops; p.slots = nc.slots; }
-            p.fa.u_start = (uint64_t)u;
-            p.fa.n_runs = (uint32_t)runs;
-            p.ga = gbase;
-            if (!cb(p)) return;
-            u += runs;
+        // Tail split (opt.fine_tail): the last runs of a full-L bucket at L - 1, so that their
+        // short workgroups can back-fill the drain of the coarse launches (streams = 2).
+        unsigned __int128 U_split = U1p;  // coarse runs [U0, U_split), then the tail at L - 1
+        int Lf = 0, Jf = 0, modef = 0, nbf = 1;
+        FastArgs faf;
+        if (opt.fine_tail && L == opt.lower_digits && L >= 2) {
+            const unsigned __int128 tail_runs = opt.fine_tail / (uint64_t)R;
+            if (tail_runs >= 1 && (U1p - U0) > 4 * tail_runs && make_fast_args(pre, d, L - 1, &Jf, &modef, &nbf, &faf)) {
+                U_split = U1p - tail_runs;
+                Lf = L - 1;
+            }
         }
+        auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, int Lx, int Jx, int modex, int nbx,
+                             const FastArgs& fax) -> bool {  // runs [ua, ub) of 10^Lx nonces
+            const unsigned __int128 Rx = kPow10[Lx];
+            const uint64_t max_runs =
+                std::max<uint64_t>(1u, std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx));
+            for (unsigned __int128 u = ua; u < ub;) {
+                const unsigned __int128 left = ub - u;
+                const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
+                Piece p;
+                memset(&p, 0, sizeof p);
+                p.first = (uint64_t)(u * Rx);
+                p.count = (uint64_t)((unsigned __int128)runs * Rx);
+                p.kind = 0;
+                p.digits = d;
+                p.L = Lx;
+                p.J = Jx;
+                p.mode = modex;
+                p.blocks = nbx;
+                p.fa = fax;
+                { const NonceCost nc = nonce_cost(Jx, modex); p.ops = nc.ops; p.slots = nc.slots; }
+                p.fa.u_start = (uint64_t)u;
+                p.fa.n_runs = (uint32_t)runs;
+                p.ga = gbase;
+                if (!cb(p)) return false;
+                u += runs;
+            }
+            return true;
+        };
+        if (!emit_runs(U0, U_split, L, J, mode, nb, fa)) return;
+        if (U_split < U1p && !emit_runs(U_split * 10u, U1p * 10u, Lf, Jf, modef, nbf, faf)) return;
         if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
     }
     flush_generic();

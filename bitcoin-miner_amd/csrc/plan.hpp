@@ -63,7 +63,14 @@ struct PlanOpts {
     // order; 2 = the pieces at the full L (coarse: 1,000-nonce lanes) on a high-priority
     // stream, the others (shorter lanes, generic edges) on a low-priority one, so that the
     // short workgroups back-fill the coarse launch's tail instead of each launch draining alone.
-    int streams = 1;
+    // Tail split: the last fine_tail nonces (whole runs) of every bucket planned at the full L
+    // go out as one more piece at L - 1 -- 100-nonce lanes whose workgroups end ~10x sooner --
+    // so that the coarse launch's drain has short work to back-fill.  0: off.
+    // Round 3 (profiles/r03d_*): 2 streams + a 2^28-nonce tail against one stream,
+    // wall clock, A/B in one process: configs[1] +1.6%, configs[2] +1.0% / +1.1%, an 8-GPU
+    // configs[3] shard +0.2%, and the predicted 8-GPU per-GPU efficiency 0.982 -> 1.00.
+    int streams = 2;
+    uint64_t fine_tail = 1ull << 28;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

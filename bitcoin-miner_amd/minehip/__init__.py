@@ -101,12 +101,15 @@ def profile_read(dev=0):
 
 
 def profile_kernels(dev=0):
-    """Per fast_search<J, MODE> variant: launches, nonces, ns, ops (largest ns first)."""
-    buf = (mh_kernel_stat * 64)()
-    n = lib.mh_profile_kernels(dev, buf, 64)
+    """Per fast_search<J, MODE> variant and lane length L (lo_digits): launches, nonces, ns, ops
+    (largest ns first).  `name` is the kernel's name in a rocprofv3 trace (the same for every L)."""
+    cap = 256
+    buf = (mh_kernel_stat * cap)()
+    n = lib.mh_profile_kernels(dev, buf, cap)
     if n < 0:
         _check(n)
-    out = [{f: int(getattr(buf[i], f)) for f, _ in mh_kernel_stat._fields_} for i in range(min(n, 64))]
+    out = [{f: int(getattr(buf[i], f)) for f, _ in mh_kernel_stat._fields_ if f != "reserved"}
+           for i in range(min(n, cap))]
     for k in out:
         k["name"] = f"mh::fast_search<{k['word']}, {k['mode']}>"
     return sorted(out, key=lambda k: -k["ns"])

@@ -50,7 +50,7 @@ class mh_piece(ctypes.Structure):
 class mh_kernel_stat(ctypes.Structure):
     _fields_ = [("word", ctypes.c_int32), ("mode", ctypes.c_int32), ("launches", ctypes.c_uint64),
                 ("nonces", ctypes.c_uint64), ("ns", ctypes.c_uint64), ("ops", ctypes.c_uint64),
-                ("slots", ctypes.c_uint64)]
+                ("slots", ctypes.c_uint64), ("lo_digits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class mh_message(ctypes.Structure):

@@ -56,7 +56,7 @@ extern "C" {
 #define MH_MAX_MSG_LEN (1u << 20)
 
 /* ABI version of this header, returned by mh_abi_version(). */
-#define MH_ABI_VERSION 2
+#define MH_ABI_VERSION 3
 
 int mh_abi_version(void);
 
@@ -147,12 +147,15 @@ int mh_profile_enable(int dev, int on);
  * n = number of slots the caller provides (<= 8). */
 int mh_profile_read(int dev, uint64_t *out, int n);
 
-/* Per fast_search<J, MODE> variant counters since mh_profile_enable(dev, 1);
- * the roofline's "dominant kernel" is the variant with the largest ns.  The
- * kernel name in a rocprofv3 trace is `mh::fast_search<word, mode>`. */
+/* Per fast_search<J, MODE> variant and lane length L (lo_digits: 10^L
+ * nonces per lane) counters since mh_profile_enable(dev, 1); the roofline's
+ * "dominant kernel" is the entry with the largest ns.  The kernel name in a
+ * rocprofv3 trace is `mh::fast_search<word, mode>` for every L (the trace
+ * tells the launches apart by grid size).  ABI 3 appended lo_digits. */
 typedef struct mh_kernel_stat {
     int32_t word, mode;
     uint64_t launches, nonces, ns, ops, slots;
+    int32_t lo_digits, reserved;
 } mh_kernel_stat;
 
 /* Writes up to cap variants that ran; returns how many ran (or MH_E*). */

@@ -46,7 +46,7 @@ def test_product_library_has_no_dev_hooks():
 
 
 def test_abi_version_and_devices():
-    assert minehip.lib.mh_abi_version() == 2
+    assert minehip.lib.mh_abi_version() == 3
     assert minehip.device_count() >= 0
 
 
@@ -134,6 +134,19 @@ def test_plan_covers_exactly():
             check_plan(m, lo, hi)
 
 
+def test_plan_fine_tail_covers_exactly(monkeypatch):
+    """MINEHIP_FINE_TAIL: the last runs of each full-L bucket are re-planned at L - 1 (a piece of
+    100-nonce lanes); the plan still tiles the range exactly, for every layout."""
+    monkeypatch.setenv("MINEHIP_FINE_TAIL", str(1 << 28))
+    for m in (b"cmu440", b"x" * 60, b"a" * 100, b"y" * 52, b"z" * 62):
+        pieces = check_plan(m, 0, 2 ** 34 - 1)
+        coarse = {p["digits"] for p in pieces if p["kind"] == 0 and p["lo_digits"] == 3}
+        tails = [p for p in pieces if p["kind"] == 0 and p["lo_digits"] == 2 and p["digits"] in coarse]
+        assert tails and all(p["count"] <= 1 << 28 for p in tails)
+        check_plan(m, 549755813888, 549755813888 + 6871947673)
+        check_plan(m, U64 - (1 << 33), U64)
+
+
 def test_plan_uses_fast_kernel_for_bulk():
     pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
     fast = sum(p["count"] for p in pieces if p["kind"] == 0)
@@ -157,15 +170,18 @@ def test_plan_coalesces_small_buckets():
 
 def test_plan_launch_cap():
     """PlanOpts: at most 2^34 nonces and 131,072 workgroups of 256 lanes per fast launch, and
-    configs[3]'s big buckets run 1,000-nonce lanes (L = 3) in launches near the nonce cap."""
+    configs[3]'s big buckets run 1,000-nonce lanes (L = 3) in launches near the nonce cap, each
+    bucket ending in one tail piece of <= 2^28 nonces at L = 2 (the default fine_tail)."""
     pieces = check_plan(b"cmu440", 0, 2 ** 40 - 1)
     fast = [p for p in pieces if p["kind"] == 0]
     assert max(p["count"] for p in pieces) <= 2 ** 34
     for p in fast:
         assert -(-(p["count"] // 10 ** p["lo_digits"]) // 256) <= 131072
-    big = [p for p in fast if p["digits"] >= 11]
-    assert big and all(p["lo_digits"] == 3 for p in big)
-    assert max(p["count"] for p in big) > 2 ** 33
+    for d in (11, 12, 13):
+        b = [p for p in fast if p["digits"] == d]
+        assert [p["lo_digits"] for p in b] == [3] * (len(b) - 1) + [2]
+        assert b[-1]["count"] <= 2 ** 28 and b[-1]["count"] > 2 ** 27
+        assert max(p["count"] for p in b) > 2 ** 33
 
 
 # ---- bitcoin.Message codec (Go encoding/json bytes) ------------------------

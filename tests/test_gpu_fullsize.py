@@ -94,7 +94,8 @@ def test_plan_knobs_full_size(gpu):
     for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1 << 18),
                dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0),
                dict(MINEHIP_STREAMS=2), dict(MINEHIP_STREAMS=2, MINEHIP_LAUNCH_NONCES=1 << 30,
-                                             MINEHIP_MAX_BLOCKS=1 << 12)):
+                                             MINEHIP_MAX_BLOCKS=1 << 12),
+               dict(MINEHIP_STREAMS=2, MINEHIP_FINE_TAIL=1 << 28), dict(MINEHIP_FINE_TAIL=(1 << 30) + 12345)):
         with env(**kv):
             assert gpu.search(msg, 0, (1 << 32) - 1) == exp, kv
 
@@ -105,7 +106,8 @@ def test_plan_knobs_two_block_layouts(gpu, name):
     bucket on the fast kernels: the answer stays the fixture's."""
     msg, lo, hi, _, result, _ = fixture(name)
     for kv in (dict(MINEHIP_LOWER_DIGITS=1), dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1 << 18),
-               dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0)):
+               dict(MINEHIP_LAUNCH_NONCES=1 << 28), dict(MINEHIP_GENERIC_BELOW=0),
+               dict(MINEHIP_STREAMS=2, MINEHIP_FINE_TAIL=1 << 28, MINEHIP_MIN_LANES=1 << 18)):
         with env(**kv):
             assert gpu.search(msg, lo, hi) == result, kv
 

@@ -169,10 +169,10 @@ def test_plan_invariance_small(gpu):
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 2, 3, 4, 5):
             for gb in (0, 1 << 20):
-                for st in (1, 2):
+                for st, ft in ((1, 0), (2, 0), (2, 20_000), (1, 99_999)):
                     with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
-                             MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st):
-                        assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st)
+                             MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft):
+                        assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st, ft)
         # tiny grids: many launches per bucket and many partial-buffer flushes (on both streams)
         for mb in (1, 3, 1000):
             for st in (1, 2):

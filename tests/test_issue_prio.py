@@ -62,9 +62,11 @@ def test_outside_kernels_untouched():
 
 
 def test_classes():
-    for op, c in (("v_alignbit_b32", "H"), ("v_add3_u32", "H"), ("v_lshrrev_b32_e64", "H"),
+    # measured on MI355X (profiles/r01d_valu_ops.json, r03b_valu_ops.json)
+    for op, c in (("v_alignbit_b32", "H"), ("v_add3_u32", "H"), ("v_lshrrev_b32_e64", "F"),
                   ("v_add_u32_e32", "F"), ("v_bitop3_b32", "F"), ("v_lshrrev_b32_e32", "F"),
-                  ("v_cndmask_b32_e64", "H"), ("v_cndmask_b32_e32", "F")):
+                  ("v_lshlrev_b32_e32", "H"), ("v_cndmask_b32_e64", "H"), ("v_cndmask_b32_e32", "H"),
+                  ("v_and_b32_e32", "F"), ("v_min_u32_dpp", "H"), ("v_cmp_lt_u32_e32", "H")):
         assert issue_prio.valu_class(f"\t{op} v1, v2, v3") == c, op
     assert issue_prio.valu_class("\ts_add_u32 s0, s1, s2") is None
 

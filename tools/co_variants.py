@@ -1,0 +1,63 @@
+"""Code-object variants of the product fast_search build for A/Bs through the dev
+build's MINEHIP_DEV_CODE_OBJECT hook (round 3):
+
+  padN   N s_nop 0 at every fast_search kernel's entry: the whole kernel body,
+         per-nonce loop included, moves by 4N bytes against instruction-cache
+         lines (the loop header is not aligned by the compiler)
+  cmpH   the per-nonce loop's v_cmp_ge_u32_e32 classed half rate (measured:
+         v_cmp_lt_u32_e32 issues at 62 lanes/clk/CU, profiles/r03b_valu_ops.json)
+
+  python tools/co_variants.py pad0 pad1 pad4 cmpH   # -> build/ab/<variant>.hsaco
+"""
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd", "csrc"))
+import issue_prio  # noqa: E402
+import valu_rates  # noqa: E402
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def assemble(text, out):
+    s = out[:-6] + ".s"
+    open(s, "w").write(text)
+    o = out[:-6] + ".o"
+    subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                    "-o", o, s], check=True)
+    subprocess.run([f"{LLVM}/ld.lld", "-shared", "-o", out, o], check=True)
+
+
+def pad(text, n):
+    return re.sub(r"^(_ZN2mh11fast_search\S+:.*)$", lambda m: m.group(1) + "\n" + "\ts_nop 0\n" * n,
+                  text, flags=re.M)
+
+
+def main():
+    src = open(os.path.join(ROOT, "build", "fast_search.s")).read()
+    os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
+    for v in sys.argv[1:]:
+        out = os.path.join(ROOT, "build", "ab", v + ".hsaco")
+        if v.startswith("pad"):
+            text, _ = issue_prio.annotate(src)
+            text = pad(text, int(v[3:]))
+        elif v == "cmpH":
+            cmps = {o for o in valu_rates.FULL if o.startswith("v_cmp_")}
+            old = valu_rates.FULL, valu_rates.HALF
+            issue_prio.valu_rate.__globals__["FULL"] = valu_rates.FULL - cmps
+            issue_prio.valu_rate.__globals__["HALF"] = valu_rates.HALF | cmps
+            try:
+                text, _ = issue_prio.annotate(src)
+            finally:
+                issue_prio.valu_rate.__globals__["FULL"], issue_prio.valu_rate.__globals__["HALF"] = old
+        else:
+            sys.exit(f"unknown variant {v}")
+        assemble(text, out)
+        print(out)
+
+
+if __name__ == "__main__":
+    main()
