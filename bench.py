@@ -257,7 +257,7 @@ def pmc_counters(msg, pieces, dev, timeout=90, passes=PMC_PASSES):
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"
     names = [f"fast_search<{p['word']}, {p['mode']}>" for p in pieces]
-    ranges = [f"{p['first']}:{p['first'] + p['count'] - 1}" for p in pieces]
+    ranges = [f"{p['first']}:{p['first'] + p['count'] - 1}:{p['lo_digits']}" for p in pieces]
     vals = {n: {} for n in names}
     work = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
@@ -348,7 +348,9 @@ def die(msg, code=2):
 
 
 def kernel_totals(per_dev_kstats):
-    """Sum the per-(variant, lane length) HIP-event stats over devices; largest time first."""
+    """Sum the per-(variant, lane length) HIP-event stats over devices; most algorithmic work
+    (nonces x nonce_ops) first.  Not by time: with two streams a back-filling
+    launch's HIP-event span includes its wait for free CUs, so its time overstates its share."""
     tot = {}
     for ks in per_dev_kstats:
         for k in ks:
@@ -356,7 +358,7 @@ def kernel_totals(per_dev_kstats):
                                dict(k, launches=0, nonces=0, ns=0, ops=0, slots=0))
             for f in ("launches", "nonces", "ns", "ops", "slots"):
                 t[f] += k[f]
-    return sorted(tot.values(), key=lambda k: -k["ns"])
+    return sorted(tot.values(), key=lambda k: -k["ops"])
 
 
 def roofline(kst, cus, n_devices, resources=None):

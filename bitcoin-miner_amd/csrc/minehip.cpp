@@ -92,6 +92,7 @@ struct DevCtx {
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
+    std::vector<mh::Piece> plan;  // the current search's pieces (reused)
     int used = 0;
     uint64_t cnt[8] = {0};
     VarStat var[kVariants];
@@ -194,10 +195,11 @@ int flush_partials(DevCtx* c, bool split) {
 // Enqueue one piece on the context's stream.  Its workgroups write their
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
-int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
-    const bool split = opt.streams == 2;
-    // streams = 2: coarse pieces (the full L) on the high-priority stream, the rest on the low one
-    hipStream_t s = !split ? c->stream : (p.kind == 0 && p.L == opt.lower_digits) ? c->s_hi : c->s_lo;
+bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) { return p.kind == 0 && p.L == opt.lower_digits; }
+
+int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
+    // split: coarse pieces (the full L) on the high-priority stream, the rest on the low one
+    hipStream_t s = !split ? c->stream : coarse_piece(p, opt) ? c->s_hi : c->s_lo;
     uint32_t blocks;
     if (p.kind == 0) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
@@ -299,7 +301,16 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     MH_HIP(hipSetDevice(dev));
     MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
     const mh::PlanOpts opt = plan_opts();
-    const bool split = opt.streams == 2;
+    c->plan.clear();
+    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
+        c->plan.push_back(p);
+        return true;
+    });
+    // Two streams only when there is something to overlap: coarse pieces and others.  A small
+    // search (generic edges, short-lane buckets) stays on one stream and skips the events.
+    bool any_coarse = false, any_fine = false;
+    for (const auto& p : c->plan) (coarse_piece(p, opt) ? any_coarse : any_fine) = true;
+    const bool split = opt.streams == 2 && any_coarse && any_fine;
     if (split) {  // both piece streams start after the reset (and after the previous search)
         MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
         MH_HIP(hipStreamWaitEvent(c->s_hi, c->ev_join[2], 0));
@@ -307,10 +318,10 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     }
     int err = MH_OK;
     c->poff = 0;
-    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
-        err = enqueue_piece(c, p, opt);
-        return err == MH_OK;
-    });
+    for (const auto& p : c->plan) {
+        err = enqueue_piece(c, p, opt, split);
+        if (err) break;
+    }
     if (!err) err = flush_partials(c, split);
     if (err) {
         (void)hipStreamSynchronize(c->s_hi);
