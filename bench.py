@@ -342,6 +342,37 @@ def gpu_config1(search_dev):
     return {"config1_ms": round(sorted(ts)[5] * 1e3, 3), "config1_result": list(r)}
 
 
+def power_sample(search_dev, dev=0, seconds=1.0):
+    """amd-smi's socket power and GFX clocks sampled once while a ~1.5 s search runs (N = 1,
+    after the timed region).  The kernel is VALU-bound at the package power limit, so power
+    and clock are what differ between boxes.  None without amd-smi."""
+    import re
+    import threading
+    smi = shutil.which("amd-smi")
+    if not smi:
+        return None
+    t = threading.Thread(target=lambda: search_dev("cmu440", 10 ** 11, 10 ** 11 + (1 << 36) - 1))
+    t.start()
+    time.sleep(seconds)
+    out = {}
+    try:
+        m = subprocess.run([smi, "metric", "--power", "--clock", "-g", str(dev)], capture_output=True,
+                           text=True, timeout=20).stdout
+        lim = subprocess.run([smi, "static", "--limit", "-g", str(dev)], capture_output=True, text=True,
+                             timeout=20).stdout
+    except (OSError, subprocess.TimeoutExpired):
+        m, lim = "", ""
+    t.join()
+    for k, v in re.findall(r"(\w*POWER\w*):\s*([\d.]+)\s*W", m + "\n" + lim):
+        out.setdefault(k.lower() + "_w", float(v))
+    gfx = [float(v) for v in re.findall(r"GFX_\d+:\s*\n\s*CLK:\s*([\d.]+)\s*MHz", m)]
+    if gfx:
+        out["gfx_clk_mhz_mean"] = round(sum(gfx) / len(gfx), 1)
+        out["gfx_clk_mhz"] = gfx
+    out["note"] = "amd-smi metric/static, one sample during a 2^36-nonce search after the timed region"
+    return out
+
+
 def die(msg, code=2):
     print(f"bench.py: {msg}", file=sys.stderr, flush=True)
     sys.exit(code)
@@ -609,6 +640,8 @@ def main():
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             cpu = cpu_baseline(cfg["msg"], threads)
             cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, devs[0]))
+        if n_gpus == 1 and not launched and not args.no_pmc:
+            roof["power"] = power_sample(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
         per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
