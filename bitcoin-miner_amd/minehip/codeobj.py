@@ -10,8 +10,6 @@ with one map per kernel: .vgpr_count, .sgpr_count, .agpr_count,
 import ctypes
 import struct
 
-import msgpack
-
 from ._lib import lib
 
 NT_AMDGPU_METADATA = 32
@@ -26,6 +24,61 @@ def fast_code_object():
     b = ctypes.addressof(ctypes.c_ubyte.in_dll(lib, "mh_fast_co_begin"))
     e = ctypes.addressof(ctypes.c_ubyte.in_dll(lib, "mh_fast_co_end"))
     return ctypes.string_at(b, e - b)
+
+
+def unpack_msgpack(b):
+    """Decode one MessagePack object (the subset AMDGPU metadata uses: maps, arrays, strings,
+    binary, integers, floats, booleans, nil).  No dependency on the msgpack package."""
+    def rd(i):
+        t = b[i]
+        if t <= 0x7F:
+            return t, i + 1
+        if t >= 0xE0:
+            return t - 0x100, i + 1
+        if 0x80 <= t <= 0x8F:
+            return rd_map(i + 1, t & 0x0F)
+        if 0x90 <= t <= 0x9F:
+            return rd_arr(i + 1, t & 0x0F)
+        if 0xA0 <= t <= 0xBF:
+            n = t & 0x1F
+            return b[i + 1:i + 1 + n].decode(), i + 1 + n
+        if t == 0xC0:
+            return None, i + 1
+        if t in (0xC2, 0xC3):
+            return t == 0xC3, i + 1
+        if t in (0xC4, 0xC5, 0xC6, 0xD9, 0xDA, 0xDB):      # bin8/16/32, str8/16/32
+            w = {0xC4: 1, 0xC5: 2, 0xC6: 4, 0xD9: 1, 0xDA: 2, 0xDB: 4}[t]
+            n = int.from_bytes(b[i + 1:i + 1 + w], "big")
+            v = b[i + 1 + w:i + 1 + w + n]
+            return (v.decode() if t >= 0xD9 else bytes(v)), i + 1 + w + n
+        if t in (0xCA, 0xCB):
+            return struct.unpack(">f" if t == 0xCA else ">d", b[i + 1:i + (5 if t == 0xCA else 9)])[0], \
+                i + (5 if t == 0xCA else 9)
+        if 0xCC <= t <= 0xD3:                               # uint8..64, int8..64
+            w = 1 << ((t - 0xCC) % 4)
+            return int.from_bytes(b[i + 1:i + 1 + w], "big", signed=t >= 0xD0), i + 1 + w
+        if t in (0xDC, 0xDD, 0xDE, 0xDF):                   # array16/32, map16/32
+            w = 2 if t in (0xDC, 0xDE) else 4
+            n = int.from_bytes(b[i + 1:i + 1 + w], "big")
+            return (rd_arr if t < 0xDE else rd_map)(i + 1 + w, n)
+        raise ValueError(f"msgpack type 0x{t:02x} not supported")
+
+    def rd_arr(i, n):
+        out = []
+        for _ in range(n):
+            v, i = rd(i)
+            out.append(v)
+        return out, i
+
+    def rd_map(i, n):
+        out = {}
+        for _ in range(n):
+            k, i = rd(i)
+            v, i = rd(i)
+            out[k] = v
+        return out, i
+
+    return rd(0)[0]
 
 
 def metadata(co):
@@ -44,7 +97,7 @@ def metadata(co):
             name = co[p + 12:p + 12 + namesz].rstrip(b"\0")
             d = p + 12 + ((namesz + 3) & ~3)
             if name == b"AMDGPU" and ntype == NT_AMDGPU_METADATA:
-                return msgpack.unpackb(co[d:d + descsz], raw=False, strict_map_key=False)
+                return unpack_msgpack(co[d:d + descsz])
             p = d + ((descsz + 3) & ~3)
     raise ValueError("no NT_AMDGPU_METADATA note")
 

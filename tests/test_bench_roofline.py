@@ -85,3 +85,16 @@ def test_resources_from_the_embedded_code_object():
     assert line["resources"]["vgpr"] == res[(4, 0)]["vgpr"]
     assert codeobj.max_waves_per_simd(69) == 7 and codeobj.max_waves_per_simd(64) == 8
     assert codeobj.max_waves_per_simd(97) == 4 and codeobj.max_waves_per_simd(129) == 3
+
+
+def test_msgpack_decoder_matches_the_msgpack_package():
+    """codeobj's own MessagePack decoder (no dependency) against the msgpack package, on the
+    embedded code object's metadata note and on a synthetic object with every type it handles."""
+    msgpack = pytest.importorskip("msgpack")
+    obj = {"a": [1, -1, 127, 128, -33, 65535, 2 ** 40, -(2 ** 40), 1.5, True, False, None],
+           "s" * 40: "x" * 300, "b": b"\x00\x01", "m": {str(i): i for i in range(20)}, "l": list(range(40))}
+    assert codeobj.unpack_msgpack(msgpack.packb(obj, use_bin_type=True)) == obj
+    co = codeobj.fast_code_object()
+    md = codeobj.metadata(co)
+    assert md["amdhsa.target"].startswith("amdgcn-amd-amdhsa--gfx950")
+    assert len(md["amdhsa.kernels"]) == 22
