@@ -427,6 +427,9 @@ def roofline(kst, cus, n_devices, resources=None):
         "unit": "T int32 VALU lane-instructions/s per GPU",
         "frac": round(achieved / peak, 4),
         "frac_at_sclk": None,                    # against the peak at the clock the kernel ran at (PMC)
+        # a kernel issues at least nonce_ops instructions per nonce, so frac > 1 would mean it skipped
+        # work (or the HIP events mis-timed it): flagged, never hidden
+        "frac_physical": achieved / peak <= 1.0,
         "basis": "algorithmic work per nonce = nonce_ops, the VALU instructions one nonce's SHA-256 "
                  "needs after hoisting the work a lane's nonces share (SURVEY §8(d) D4 restated for "
                  "gfx950, DESIGN.md §4), x the dominant kernel's nonces / its HIP-event launch time; "

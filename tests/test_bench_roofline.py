@@ -39,7 +39,7 @@ def test_frac_is_a_fraction_at_the_issue_limit(cfg):
     p = dominant_piece(cfg)
     line = bench.roofline([kstat(p, fastest_possible_ns(p))], CUS, 1)
     # at the fastest time the hardware allows, frac equals the mix bound, which is <= 1
-    assert line["frac"] <= 1.0
+    assert line["frac"] <= 1.0 and line["frac_physical"]
     assert line["frac"] == pytest.approx(line["mix_bound_frac"], rel=2e-3)
     assert line["frac_of_mix_bound"] == pytest.approx(1.0, rel=2e-3)
     assert line["alg_instr_per_nonce"] == p["nonce_ops"]
@@ -58,6 +58,14 @@ def test_frac_from_measured_kernel_rates(cfg):
         line = bench.roofline([kstat(p, p["count"] / ghs)], CUS, 1)
         assert 0.0 < line["frac"] < 1.0, (cfg, ghs, line["frac"])
         assert line["frac"] == pytest.approx(ghs * 1e9 * p["nonce_ops"] / 1e12 / line["peak"], rel=1e-3)
+
+
+def test_impossible_time_is_flagged():
+    """A launch timed faster than the issue limit allows (work skipped, or a broken timer) gives
+    frac > 1 and frac_physical False -- reported, not clipped."""
+    p = dominant_piece("2")
+    line = bench.roofline([kstat(p, fastest_possible_ns(p) * 0.5)], CUS, 1)
+    assert line["frac"] > 1.0 and not line["frac_physical"]
 
 
 def test_frac_recomputes_from_a_kernel_trace():
