@@ -645,6 +645,12 @@ def main():
             cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, devs[0]))
         if n_gpus == 1 and not launched and not args.no_pmc:
             roof["power"] = power_sample(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
+            if roof["power"] and roof["power"].get("gfx_clk_mhz_mean"):
+                # amd-smi's clock of an un-profiled run reads at or above the in-kernel clock, the
+                # PMC pass's (a profiled run) at or below it (MI355X_MICROARCH.md "DVFS give-back"):
+                # the two fractions bracket the kernel's share of the peak at the clock it ran at
+                smi = roof["power"]["gfx_clk_mhz_mean"] * 1e6
+                roof["frac_at_smi_clk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * smi / 1e12), 4)
         per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
