@@ -92,7 +92,6 @@ struct DevCtx {
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
-    std::vector<mh::Piece> plan;  // the current search's pieces (reused)
     int used = 0;
     uint64_t cnt[8] = {0};
     VarStat var[kVariants];
@@ -301,15 +300,16 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     MH_HIP(hipSetDevice(dev));
     MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
     const mh::PlanOpts opt = plan_opts();
-    c->plan.clear();
-    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
-        c->plan.push_back(p);
-        return true;
-    });
     // Two streams only when there is something to overlap: coarse pieces and others.  A small
-    // search (generic edges, short-lane buckets) stays on one stream and skips the events.
+    // search (generic edges, short-lane buckets) stays on one stream and skips the events.  The
+    // plan is streamed, never stored (a range can hold ~2^30 pieces); this first pass stops as
+    // soon as it has seen both kinds.
     bool any_coarse = false, any_fine = false;
-    for (const auto& p : c->plan) (coarse_piece(p, opt) ? any_coarse : any_fine) = true;
+    if (opt.streams == 2)
+        mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
+            (coarse_piece(p, opt) ? any_coarse : any_fine) = true;
+            return !(any_coarse && any_fine);
+        });
     const bool split = opt.streams == 2 && any_coarse && any_fine;
     if (split) {  // both piece streams start after the reset (and after the previous search)
         MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
@@ -318,10 +318,10 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     }
     int err = MH_OK;
     c->poff = 0;
-    for (const auto& p : c->plan) {
+    mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
         err = enqueue_piece(c, p, opt, split);
-        if (err) break;
-    }
+        return err == MH_OK;
+    });
     if (!err) err = flush_partials(c, split);
     if (err) {
         (void)hipStreamSynchronize(c->s_hi);
