@@ -109,10 +109,24 @@ def step_range(cfg, k, steps):
     return split(0, (1 << cfg["bits"]) - 1, steps, k % steps)
 
 
-def rank_range(cfg, rank, world, k=0, steps=1):
-    """This rank's shard of step k."""
+def weighted_split(lo, hi, weights, i):
+    """The i-th of len(weights) contiguous pieces of [lo, hi], piece j sized in proportion to
+    the integer weights[j] (None if empty).  Exact integer arithmetic: the pieces tile [lo, hi]."""
+    n = hi - lo + 1
+    tot = sum(weights)
+    before = sum(weights[:i])
+    a = lo + n * before // tot
+    b = lo + n * (before + weights[i]) // tot - 1
+    return (a, b) if b >= a else None
+
+
+def rank_range(cfg, rank, world, k=0, steps=1, weights=None):
+    """This rank's shard of step k.  Strong steps are split equally, or in proportion to
+    `weights` (one integer per rank, Balancer.weights) when given."""
     if cfg["scaling"] == "weak":
         return shard(rank, cfg["bits"])
+    if weights is not None:
+        return weighted_split(*step_range(cfg, k, steps), weights, rank)
     return split(*step_range(cfg, k, steps), world, rank)
 
 
@@ -128,15 +142,75 @@ def merge(results):
     return min(results)
 
 
-def host_merge(r, world, dist):
-    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors)."""
+def host_merge_stats(r, world, dist, nonces=0, ns=0):
+    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors), with each
+    rank's (nonces searched, search ns) of the step riding in the same all_gather.
+    Returns (merged tuple, [(nonces, ns) per rank])."""
     if world == 1:
-        return r
+        return r, [(nonces, ns)]
     import torch
-    t = torch.tensor([r[0] - (1 << 63), r[1] - (1 << 63)], dtype=torch.int64)  # u64 -> i64, order kept
+    t = torch.tensor([r[0] - (1 << 63), r[1] - (1 << 63), nonces, ns], dtype=torch.int64)  # u64 -> i64, order kept
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t)
-    return merge(tuple(int(v) + (1 << 63) for v in o.tolist()) for o in out)
+    vals = [o.tolist() for o in out]
+    return merge((v[0] + (1 << 63), v[1] + (1 << 63)) for v in vals), [(v[2], v[3]) for v in vals]
+
+
+def host_merge(r, world, dist):
+    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors)."""
+    return host_merge_stats(r, world, dist)[0]
+
+
+class Balancer:
+    """Strong-scaling shard sizes in proportion to each rank's measured search rate.
+
+    Equal shards make every strong step as slow as the slowest GPU, and MI355X
+    devices run this power-limited kernel at clocks that differ by several
+    percent.  Each rank's (nonces, search ns) of a step ride
+    in that step's merge all_gather, so every rank holds the same cumulative
+    rates and computes the same split: no extra collective, and the K steps
+    still tile the job range exactly once.  The first step a rank sees (device
+    context and module load) is not counted."""
+
+    SCALE = 1 << 20
+
+    def __init__(self, world, enabled=True):
+        self.world = world
+        self.enabled = enabled and world > 1
+        self.nonces = [0] * world
+        self.ns = [0] * world
+        self.steps_seen = 0
+
+    def update(self, stats):
+        self.steps_seen += 1
+        if self.steps_seen == 1:
+            return
+        for i, (n, t) in enumerate(stats):
+            self.nonces[i] += n
+            self.ns[i] += t
+
+    def weights(self):
+        """Integer weights (one per rank, max SCALE), or None for equal shards."""
+        if not self.enabled or any(n <= 0 or t <= 0 for n, t in zip(self.nonces, self.ns)):
+            return None
+        rates = [n / t for n, t in zip(self.nonces, self.ns)]
+        top = max(rates)
+        return [max(1, round(self.SCALE * x / top)) for x in rates]
+
+
+def launched_step(search, cfg, rank, world, k, steps, dist, bal=None):
+    """One step of the launched (one process per GPU) path: this rank's shard of step k
+    (rate-weighted when `bal` has rates), searched with search(lo, hi), then the host
+    merge.  Returns (merged (hash, nonce), nonces this rank searched)."""
+    rr = rank_range(cfg, rank, world, k, steps, bal.weights() if bal is not None else None)
+    t0 = time.perf_counter_ns()
+    r = search(rr[0], rr[1]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
+    dt = time.perf_counter_ns() - t0
+    n = rr[1] - rr[0] + 1 if rr else 0
+    merged, stats = host_merge_stats(r, world, dist, n, dt)
+    if bal is not None:
+        bal.update(stats)
+    return merged, n
 
 
 def run_timed(step, steps, warmup, barrier, sync):
@@ -542,13 +616,16 @@ def main():
     done = {d: 0 for d in devs}  # nonces searched per device in the timed region
     uniq = sorted(set(devs))
 
+    # strong steps at N > 1: shards in proportion to each rank's measured rate (BENCH_BALANCE=0: equal)
+    bal = Balancer(world, cfg["scaling"] == "strong" and os.environ.get("BENCH_BALANCE", "1") != "0")
+
     def step(k, timed=False):
         if launched:
-            rr = rank_range(cfg, rank, world, k, steps)
-            r = minehip.search(msg, rr[0], rr[1], devs[0]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
-            if timed and rr:
-                done[devs[0]] += rr[1] - rr[0] + 1
-            return host_merge(r, world, dist)
+            r, n = launched_step(lambda a, b: minehip.search(msg, a, b, devs[0]),
+                                 cfg, rank, world, k, steps, dist, bal)
+            if timed:
+                done[devs[0]] += n
+            return r
         lo, hi = job_range(cfg, n_gpus, k, steps)
         if multi:
             return minehip.search_multi(msg, lo, hi, devs)
@@ -684,6 +761,9 @@ def main():
                            "one process, mh_search_multi: one host thread + HIP stream per device" if multi else
                            "one process, mh_search on one device"),
                 "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
+                "shards": ("each strong step split in proportion to every rank's measured search rate "
+                           "(gathered with the step's merge)" if launched and bal.enabled else
+                           "scheduler chunks sized to each device's rate" if multi else "equal"),
             },
             "per_device": per_device,
             "roofline": roof,

@@ -15,6 +15,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 import torch.distributed as dist
@@ -35,48 +36,101 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cfg, steps, q):
+def _worker(rank, world, port, cfg, steps, q, balance=False, slow_ns=0, warmup=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mine = []
+    bal = bench.Balancer(world, balance)
+
+    def search(a, b):
+        mine.append((a, b))
+        r = oracle.search(MSG, a, b)
+        if slow_ns:  # a slower device: rank r takes (r + 1) x slow_ns per nonce
+            time.sleep((b - a + 1) * slow_ns * (rank + 1) * 1e-9)
+        return r
 
     def step(k):
-        rr = bench.rank_range(cfg, rank, world, k, steps)
-        mine.append(rr)
-        r = oracle.search(MSG, rr[0], rr[1]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
-        return bench.host_merge(r, world, dist)
+        return bench.launched_step(search, cfg, rank, world, k, steps, dist, bal)[0]
 
-    r, elapsed = bench.run_timed(step, steps, 1, dist.barrier, lambda: None)
+    r, elapsed = bench.run_timed(step, steps, warmup, dist.barrier, lambda: None)
     import torch
     t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    q.put((rank, r, float(t.item()), mine[1:]))  # mine[0] is the warmup step
+    q.put((rank, r, float(t.item()), mine[warmup:], bal.weights()))  # mine[:warmup]: the warmup steps
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _launch(world, cfg, steps, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, steps, q), kwargs=kw) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _tiles_once(out, lo, hi):
+    rs = sorted(r for o in out for r in o[3])
+    return rs[0][0] == lo and rs[-1][1] == hi and all(rs[i][1] + 1 == rs[i + 1][0] for i in range(len(rs) - 1))
 
 
 @pytest.mark.parametrize("world,scaling", [(2, "strong"), (3, "strong"), (2, "weak")])
 def test_sharded_merge_matches_full_scan(world, scaling):
     bits, steps = (15, 4) if scaling == "strong" else (12, 2)
     cfg = dict(msg="cmu440", bits=bits, scaling=scaling)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, steps, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=120) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = _launch(world, cfg, steps)
     lo, hi = 0, ((1 << bits) if scaling == "strong" else world << bits) - 1
     exp = oracle.search(MSG, lo, hi)
     assert all(o[1] == exp for o in out)          # every rank holds the merged min of the job
     assert len({o[2] for o in out}) == 1          # max-over-ranks time agreed
     if scaling == "strong":                       # the timed steps covered [lo, hi] exactly once
-        rs = sorted(r for o in out for r in o[3])
-        assert rs[0][0] == lo and rs[-1][1] == hi
-        assert all(rs[i][1] + 1 == rs[i + 1][0] for i in range(len(rs) - 1))
+        assert _tiles_once(out, lo, hi)
+
+
+def test_balanced_strong_shards_follow_rates():
+    """bench.py's default at N > 1 (strong steps): shards in proportion to each rank's measured
+    rate.  Rank 1 is made 2x slower per nonce; after the warmup steps it gets about a third of
+    every step, every rank computes the same weights, the timed steps still tile the job once
+    and the merged result is the full scan's."""
+    world, bits, steps = 2, 16, 4
+    cfg = dict(msg="cmu440", bits=bits, scaling="strong")
+    out = _launch(world, cfg, steps, balance=True, slow_ns=2000, warmup=3)
+    lo, hi = 0, (1 << bits) - 1
+    assert all(o[1] == oracle.search(MSG, lo, hi) for o in out)
+    assert _tiles_once(out, lo, hi)
+    assert out[0][4] == out[1][4] and out[0][4] is not None      # same weights on every rank
+    last = [o[3][-1][1] - o[3][-1][0] + 1 for o in out]          # each rank's share of the last step
+    assert 0.25 < last[1] / sum(last) < 0.42, last
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_weighted_split_tiles(world):
+    for weights in ([1] * world, list(range(1, world + 1)), [1 << 20] + [1] * (world - 1)):
+        for lo, hi in ((0, 99), (5, 5 + 10 ** 9), (0, (1 << 40) - 1)):
+            rs = [bench.weighted_split(lo, hi, weights, i) for i in range(world)]
+            rs = [r for r in rs if r]
+            assert rs[0][0] == lo and rs[-1][1] == hi
+            assert all(rs[i][1] + 1 == rs[i + 1][0] for i in range(len(rs) - 1))
+    assert bench.weighted_split(0, 99, [1, 3], 0) == (0, 24)
+    assert bench.weighted_split(0, 99, [1, 3], 1) == (25, 99)
+
+
+def test_balancer_skips_the_first_step_and_needs_every_rate():
+    b = bench.Balancer(2)
+    b.update([(100, 10 ** 9), (100, 10 ** 9)])   # first step: context / module load, not counted
+    assert b.weights() is None
+    b.update([(100, 1000), (0, 1000)])             # a rank without nonces: no rate yet
+    assert b.weights() is None
+    b.update([(100, 1000), (300, 1000)])             # cumulative: 200 / 2000 ns against 300 / 2000 ns
+    assert b.weights() == [round(bench.Balancer.SCALE * 2 / 3), bench.Balancer.SCALE]
+    assert bench.Balancer(2, enabled=False).weights() is None
+    assert bench.Balancer(1).weights() is None
 
 
 def test_merge_is_lexicographic():
