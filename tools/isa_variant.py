@@ -122,6 +122,22 @@ def variant(name, base_text):
         # pv_<minF>_<leadF>_<leadH>: marker-placement variants of the issue-priority pass
         _, mf, lf, lh = name.split("_")
         return prio_variant(base_text, int(mf), int(lf), int(lh))
+    if name.startswith("dup"):
+        # dup<k>: the product build with every k-th s_setprio written twice.  The copy changes
+        # nothing the wave does (same priority) but adds 4 bytes of code: a probe of whether
+        # instruction fetch (32-byte requests per wave from the I-cache shared by two CUs)
+        # co-limits the loop.
+        k = int(name[3:])
+        t, _ = prio_phases(base_text)
+        out, n, i = [], 0, 0
+        for line, fast in in_fast(t):
+            out.append(line)
+            if fast and re.match(r"^\s+s_setprio\s+\d+\s*$", line):
+                i += 1
+                if i % k == 0:
+                    out.append(line)
+                    n += 1
+        return "\n".join(out), n
     if name.startswith("prio"):
         return prio_phases(base_text)
     raise SystemExit(f"unknown variant {name}")
