@@ -26,7 +26,7 @@ RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
 DEVLIB  := $(BUILD)/dev/libminehip.so
 
-all: $(LIB) $(LSPLIB) $(CLIS) oracle dev
+all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so
 
 # LSP endpoint (host only, wire compatible with the reference's Go lsp package)
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
@@ -68,6 +68,11 @@ $(BIN)/minehip-%: $(APPS)/%_main.cpp $(APPS)/common.hpp include/minehip.h includ
 
 oracle:
 	$(MAKE) -s -C oracle
+
+# in-kernel clock probe (measurement only: bench.py's roofline.kernel_clock)
+$(BUILD)/libclockprobe.so: tools/clock_probe.hip
+	mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # disassembly + register report of the kernels (for DESIGN.md / profiling)
 asm: $(FAST_PS)

@@ -416,6 +416,51 @@ def gpu_config1(search_dev):
     return {"config1_ms": round(sorted(ts)[5] * 1e3, 3), "config1_result": list(r)}
 
 
+def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
+    """The engine clock the fast kernel runs at, read inside the GPU during an un-profiled
+    search (tools/clock_probe.hip, build/libclockprobe.so): one-wave probe workgroups on their
+    own stream sleep through a 2^37-nonce search of the dominant layout (fast_search<4, One> at
+    L = 3) and read the shader-clock and 100 MHz counters at both ends of a window inside it.
+    Returns the median clock over the probes, the median per XCD and the search's own rate, or
+    None when the probe library is missing or the window did not lie inside the search."""
+    import ctypes
+    path = os.path.join(ROOT, "build", "libclockprobe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.cp_start.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
+    lib.cp_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    lo, n = 10 ** 11, 1 << 37  # d = 12: last digit in word 4, the configs[1] d = 10 bucket's layout
+    if lib.cp_start(dev, delay_s, window_s, nwg) != 0:
+        return None
+    t = time.perf_counter()
+    search_dev("cmu440", lo, lo + n - 1)
+    search_s = time.perf_counter() - t
+    buf = (ctypes.c_uint64 * (4 * nwg))()
+    if lib.cp_read(buf, nwg) != 0:
+        return None
+    rows = [tuple(buf[4 * i:4 * i + 4]) for i in range(nwg)]
+    ghz = [(x, c / (k / 1e8) / 1e9) for x, c, k, _ in rows if k]
+    late = max(w for *_, w in rows) / 1e8  # window start after the workgroup started, s
+    if not ghz or search_s < late + window_s + 0.1:
+        return {"ghz": None, "note": f"probe window not inside the search ({search_s:.2f} s)"}
+
+    def med(v):
+        v = sorted(v)
+        return v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2 - 1] + v[len(v) // 2]) / 2
+
+    by_xcd = {}
+    for x, g in ghz:
+        by_xcd.setdefault(int(x), []).append(g)
+    return {"ghz": round(med([g for _, g in ghz]), 4),
+            "ghz_by_xcd": {str(x): round(med(v), 4) for x, v in sorted(by_xcd.items())},
+            "probes": len(ghz), "window_s": window_s, "search_s": round(search_s, 3),
+            "search_ghs": round(n / search_s / 1e9, 3),
+            "note": "s_memtime / s_memrealtime x 100 MHz in one-wave probe workgroups on their own stream, "
+                    f"window {delay_s}..{delay_s + window_s} s into a 2^37-nonce un-profiled search of "
+                    "fast_search<4, One> (tools/clock_probe.hip)"}
+
+
 def power_sample(search_dev, dev=0, seconds=1.0):
     """amd-smi's socket power and GFX clocks sampled once while a ~1.5 s search runs (N = 1,
     after the timed region).  The kernel is VALU-bound at the package power limit, so power
@@ -728,6 +773,17 @@ def main():
                 # the two fractions bracket the kernel's share of the peak at the clock it ran at
                 smi = roof["power"]["gfx_clk_mhz_mean"] * 1e6
                 roof["frac_at_smi_clk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * smi / 1e12), 4)
+            # the clock read inside the GPU during an un-profiled search of the same kernel, and the
+            # fraction of the issue peak at that clock (between frac_at_smi_clk and frac_at_sclk)
+            kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
+            if kc:
+                roof["kernel_clock"] = kc
+                if kc.get("ghz"):
+                    at = kc["ghz"] * 1e9
+                    roof["frac_at_kernel_clk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * at / 1e12), 4)
+                    if roof.get("mix_bound_frac"):
+                        roof["frac_of_mix_bound_at_kernel_clk"] = round(
+                            roof["frac_at_kernel_clk"] / roof["mix_bound_frac"], 4)
         per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)

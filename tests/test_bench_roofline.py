@@ -106,3 +106,27 @@ def test_msgpack_decoder_matches_the_msgpack_package():
     md = codeobj.metadata(co)
     assert md["amdhsa.target"].startswith("amdgcn-amd-amdhsa--gfx950")
     assert len(md["amdhsa.kernels"]) == 22
+
+
+def test_clock_probe_library_exports():
+    """bench.py's in-kernel clock probe (tools/clock_probe.hip -> build/libclockprobe.so, part of
+    `make all`): the two entry points bench.kernel_clock binds.  Loading needs no GPU."""
+    import ctypes
+    import os
+    path = os.path.join(os.path.dirname(bench.__file__), "build", "libclockprobe.so")
+    lib = ctypes.CDLL(path)
+    assert hasattr(lib, "cp_start") and hasattr(lib, "cp_read")
+    lib.cp_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    buf = (ctypes.c_uint64 * 4)()
+    assert lib.cp_read(buf, 1) == -1            # nothing started: refused, no device touched
+
+
+@pytest.mark.gpu
+def test_kernel_clock_during_a_search(gpu):
+    """The probe's clock during an un-profiled fast_search<4, One> search: one reading per probe
+    workgroup, spread over the 8 XCDs, inside MI355X's clock range."""
+    kc = bench.kernel_clock(lambda m, a, b: gpu.search(m, a, b))
+    assert kc is not None and kc["ghz"] is not None, kc
+    assert 1.0 < kc["ghz"] <= 2.5, kc
+    assert len(kc["ghz_by_xcd"]) == 8 and kc["probes"] == 64, kc
+    assert all(1.0 < g <= 2.5 for g in kc["ghz_by_xcd"].values()), kc
