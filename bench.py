@@ -39,7 +39,9 @@ per compression instead (can exceed 1).  `roofline.resources` are the kernel's
 VGPR/SGPR/scratch from the embedded code object.  At N = 1, rocprofv3 --pmc
 passes over one launch of each of the two largest kernels give HBM traffic,
 the clock (`sclk_ghz`, `roofline.frac_at_sclk`) and the SQ counters
-(`roofline.pmc`).  `cpu_baseline` times the CPU port of the reference loop
+(`roofline.pmc`); probe workgroups on their own stream read the clock inside the GPU
+during an un-profiled search (`roofline.kernel_clock`, `frac_at_kernel_clk`,
+tools/clock_probe.hip).  `cpu_baseline` times the CPU port of the reference loop
 (oracle/) on a bounded sample, at N = 1 only.
 """
 import argparse
