@@ -610,6 +610,8 @@ def main():
                          "N workers on fewer GPUs, e.g. --gpus 4 --devices 0,0,0,0 on a 1-GPU box")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--no-clock", action="store_true",
+                    help="skip the in-kernel clock probe after the timed region (tools/clock_probe.hip)")
     args = ap.parse_args()
     if args.gpus < 1 or args.steps < 1 or args.warmup < 0:
         die("--gpus and --steps must be >= 1, --warmup >= 0")
@@ -692,6 +694,12 @@ def main():
     for p in per_dev:
         p["nonces"] = done[p["dev"]] if launched else p["prof"]["fast_nonces"] + p["prof"]["generic_nonces"]
         p["elapsed"] = elapsed
+    if launched and not args.no_clock:
+        # every rank's own GPU clock, read inside the GPU during an un-profiled search run by all
+        # ranks at once after the timed region: what sets the per-GPU rates of a multi-GPU line
+        kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
+        for p in per_dev:
+            p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
 
     t_max = elapsed
     if launched:
@@ -775,8 +783,9 @@ def main():
                 # the two fractions bracket the kernel's share of the peak at the clock it ran at
                 smi = roof["power"]["gfx_clk_mhz_mean"] * 1e6
                 roof["frac_at_smi_clk"] = round(roof["achieved"] / (cus * LANES_PER_CU_CLK * smi / 1e12), 4)
+        if n_gpus == 1 and not launched and not args.no_clock:
             # the clock read inside the GPU during an un-profiled search of the same kernel, and the
-            # fraction of the issue peak at that clock (between frac_at_smi_clk and frac_at_sclk)
+            # fraction of the issue peak at that clock
             kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
             if kc:
                 roof["kernel_clock"] = kc
@@ -789,7 +798,8 @@ def main():
         per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
-                       if p["kstats"] and p["kstats"][0]["ns"] else None}
+                       if p["kstats"] and p["kstats"][0]["ns"] else None,
+                       "kernel_clock_ghz": p.get("kernel_clock_ghz")}
                       for p in per_dev]
         line = {
             "metric": METRIC,

@@ -74,22 +74,22 @@ for s in $STEPS; do
       ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+          -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --no-clock > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
       ;;
     pmc)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
           -d "$OUT/pmc1" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc1.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --no-clock > /dev/null 2> "$OUT/pmc1.err")
       rc=$?; echo "pmc1 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace \
           -d "$OUT/pmc2" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc2.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --no-clock > /dev/null 2> "$OUT/pmc2.err")
       rc=$?; echo "pmc2 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
           -d "$OUT/pmc3" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc > /dev/null 2> "$OUT/pmc3.err")
+          -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-pmc --no-clock > /dev/null 2> "$OUT/pmc3.err")
       rc=$?; echo "pmc3 rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       ;;
     listpmc)
