@@ -435,11 +435,14 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
     lo, n = 10 ** 11, 1 << 37  # d = 12: last digit in word 4, the configs[1] d = 10 bucket's layout
     if lib.cp_start(dev, delay_s, window_s, nwg) != 0:
         return None
-    t = time.perf_counter()
-    search_dev("cmu440", lo, lo + n - 1)
-    search_s = time.perf_counter() - t
     buf = (ctypes.c_uint64 * (4 * nwg))()
-    if lib.cp_read(buf, nwg) != 0:
+    try:
+        t = time.perf_counter()
+        search_dev("cmu440", lo, lo + n - 1)
+        search_s = time.perf_counter() - t
+    finally:
+        rc = lib.cp_read(buf, nwg)  # always: waits for the probes and frees their buffer
+    if rc != 0:
         return None
     rows = [tuple(buf[4 * i:4 * i + 4]) for i in range(nwg)]
     ghz = [(x, c / (k / 1e8) / 1e9) for x, c, k, _ in rows if k]

@@ -59,13 +59,26 @@ extern "C" int cp_start(int dev, double delay_s, double window_s, int nwg) {
     if (nwg < 1 || nwg > 4096 || delay_s < 0 || window_s <= 0 || g_out) return -1;
     if (hipSetDevice(dev) != hipSuccess) return -2;
     if (!g_stream && hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess) return -3;
-    if (hipMalloc(&g_out, sizeof(uint64_t) * 4 * nwg) != hipSuccess) return -4;
-    if (hipMemsetAsync(g_out, 0, sizeof(uint64_t) * 4 * nwg, g_stream) != hipSuccess) return -5;
+    if (hipMalloc(&g_out, sizeof(uint64_t) * 4 * nwg) != hipSuccess) {
+        g_out = nullptr;
+        return -4;
+    }
+    if (hipMemsetAsync(g_out, 0, sizeof(uint64_t) * 4 * nwg, g_stream) != hipSuccess) {
+        (void)hipFree(g_out);
+        g_out = nullptr;
+        return -5;
+    }
     g_nwg = nwg;
     g_dev = dev;
     hipLaunchKernelGGL(clock_probe, dim3(nwg), dim3(64), 0, g_stream, g_out,
                        (uint64_t)(delay_s * kRealtimeHz), (uint64_t)(window_s * kRealtimeHz));
-    return hipGetLastError() == hipSuccess ? 0 : -6;
+    if (hipGetLastError() != hipSuccess) {  // nothing runs: free the buffer so a later start works
+        (void)hipStreamSynchronize(g_stream);
+        (void)hipFree(g_out);
+        g_out = nullptr;
+        return -6;
+    }
+    return 0;
 }
 
 extern "C" int cp_read(uint64_t* out, int nwg) {
