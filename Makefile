@@ -13,7 +13,11 @@ LLVM    ?= /opt/rocm/lib/llvm/bin
 BUILD   := build
 FAST_HDRS := $(CSRC)/kernel_common.hpp $(CSRC)/layout.hpp $(CSRC)/sha256_gfx950.hpp
 FAST_S  := $(BUILD)/fast_search.s
+FAST_SP := $(BUILD)/fast_search_split.s
 FAST_PS := $(BUILD)/fast_search_prio.s
+FAST_MIX := $(BUILD)/fast_loop_mix.json
+# every ADD3_SPLIT-th v_add3 of each fast kernel as two full-rate adds (csrc/add3_split.py; 0: none)
+ADD3_SPLIT ?= 3
 FAST_CO := $(BUILD)/fast_search.hsaco
 FAST_O  := $(BUILD)/fast_co.o
 FASTFLAGS ?=
@@ -26,7 +30,7 @@ RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
 DEVLIB  := $(BUILD)/dev/libminehip.so
 
-all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so
+all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so $(FAST_MIX)
 
 # LSP endpoint (host only, wire compatible with the reference's Go lsp package)
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
@@ -43,13 +47,18 @@ $(DEVLIB): $(SRCS) $(HDRS) $(FAST_O)
 	mkdir -p $(BUILD)/dev
 	$(HIPCC) $(HIPFLAGS) -DMH_DEV_HOOKS -shared -o $@ $(SRCS) -x none $(FAST_O)
 
-# fast_search<J, MODE>: gfx950 assembly -> issue-priority pass (s_setprio around half-/full-rate
-# runs) -> code object -> embedded in the library (fast_co.S)
+# fast_search<J, MODE>: gfx950 assembly -> add3 split (every third v_add3 as two full-rate adds)
+# -> issue-priority pass (s_setprio around half-/full-rate runs) -> code object ->
+# embedded in the library (fast_co.S); the per-nonce loops' issued mix -> fast_loop_mix.json (bench)
 $(FAST_S): $(CSRC)/fast_search.hip $(FAST_HDRS)
 	mkdir -p $(BUILD)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $(FASTFLAGS) --cuda-device-only -S -o $@ $<
-$(FAST_PS): $(FAST_S) $(CSRC)/issue_prio.py $(CSRC)/valu_rates.py
+$(FAST_SP): $(FAST_S) $(CSRC)/add3_split.py
+	python3 $(CSRC)/add3_split.py $(ADD3_SPLIT) $< $@
+$(FAST_PS): $(FAST_SP) $(CSRC)/issue_prio.py $(CSRC)/valu_rates.py
 	python3 $(CSRC)/issue_prio.py $< $@
+$(FAST_MIX): $(FAST_PS) $(CSRC)/loop_mix.py $(CSRC)/valu_rates.py
+	python3 $(CSRC)/loop_mix.py $< $@
 $(FAST_CO): $(FAST_PS)
 	$(LLVM)/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c -o $(BUILD)/fast_search_prio.o $<
 	$(LLVM)/ld.lld -shared -o $@ $(BUILD)/fast_search_prio.o

@@ -516,7 +516,18 @@ def kernel_totals(per_dev_kstats):
     return sorted(tot.values(), key=lambda k: -k["ops"])
 
 
-def roofline(kst, cus, n_devices, resources=None):
+def fast_loop_mix():
+    """{(J, MODE): {"valu": N, "half": H}} of the per-nonce loops as built (build/fast_loop_mix.json,
+    written by csrc/loop_mix.py from the assembly embedded in libminehip.so), or None."""
+    try:
+        with open(os.path.join(ROOT, "build", "fast_loop_mix.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {tuple(int(x) for x in k.split(",")): v for k, v in d.items()}
+
+
+def roofline(kst, cus, n_devices, resources=None, loop_mix=None):
     """Roofline of the dominant kernel from its HIP-event launch times (summed
     over devices, so achieved is per GPU).
 
@@ -528,7 +539,13 @@ def roofline(kst, cus, n_devices, resources=None):
     instructions per nonce (PMC SQ_INSTS_VALU: 1,200.6 for fast_search<4,0>
     against nonce_ops 1,195), so frac <= the hardware's issue fraction <= 1.
     frac_survey_d4 prices every nonce at SURVEY D4's 1,616 ops x tail blocks:
-    a pricing convention that credits the hoisting and can exceed 1."""
+    a pricing convention that credits the hoisting and can exceed 1.
+
+    mix_bound_frac: the most frac can reach -- a half-rate op never shares its
+    quad-cycle with another half-rate op, so a nonce needs >= max(H, N/2)
+    quad-cycles.  With loop_mix (fast_loop_mix()) H and N are those of the
+    per-nonce loop as built (the add3 split trades half-rate ops for full-rate
+    ones); alg_mix_bound_frac is the algorithm's own mix (nonce_slots)."""
     peak = cus * LANES_PER_CU_CLK * PEAK_SCLK_HZ / 1e12
     if not kst:
         return {"bound": "valu", "achieved": None, "peak": round(peak, 3), "frac": None}
@@ -541,7 +558,10 @@ def roofline(kst, cus, n_devices, resources=None):
     n_instr = ops / nonces
     n_half = (dom["slots"] - dom["ops"]) / nonces  # slots count a half-rate op twice
     achieved = ops / sec / 1e12
-    mix = n_instr / (2 * max(n_half, n_instr / 2))
+    alg_mix = n_instr / (2 * max(n_half, n_instr / 2))
+    built = (loop_mix or {}).get((dom["word"], dom["mode"]))
+    # the loop as built issues N' >= nonce_ops instructions, H' of them half rate
+    mix = n_instr / (2 * max(built["half"], built["valu"] / 2)) if built else alg_mix
     d4 = dom["nonces"] * SURVEY_OPS_PER_COMPRESSION * blocks
     launches = max(1, dom["launches"])
     line = {
@@ -562,9 +582,14 @@ def roofline(kst, cus, n_devices, resources=None):
         "alg_instr_per_nonce": round(n_instr, 1),
         "half_rate_per_nonce": round(n_half, 1),
         # a half-rate op cannot share its quad-cycle with another half-rate op, so a nonce needs
-        # >= max(H, N/2) quad-cycles: the most this per-nonce mix can reach
+        # >= max(H, N/2) quad-cycles: the most frac can reach with the loop as built
         "mix_bound_frac": round(mix, 4),
         "frac_of_mix_bound": round(achieved / peak / mix, 4),
+        # the same bound for the algorithm's own mix (every add3 kept)
+        "alg_mix_bound_frac": round(alg_mix, 4),
+        "issued_loop": ({"valu_per_nonce": built["valu"], "half_rate_per_nonce": built["half"],
+                         "source": "build/fast_loop_mix.json (csrc/loop_mix.py over the assembly embedded "
+                                   "in libminehip.so)"} if built else None),
         "frac_survey_d4": round(d4 / sec / 1e12 / peak, 4),
         "frac_survey_d4_note": f"SURVEY §8(d) D4's {SURVEY_OPS_PER_COMPRESSION} ops per compression x "
                                f"{blocks} tail block(s) per nonce over the same time and peak: D4 prices "
@@ -724,7 +749,7 @@ def main():
     cus = int(props.multi_processor_count)
     kst = kernel_totals([p["kstats"] for p in per_dev])
     from minehip import codeobj
-    roof = roofline(kst, cus, len(per_dev), codeobj.fast_kernel_resources())
+    roof = roofline(kst, cus, len(per_dev), codeobj.fast_kernel_resources(), fast_loop_mix())
     # the whole timed region on the same basis: every fast piece's nonces x nonce_ops over the
     # max-over-ranks wall time and all N GPUs' peak -- tails, generic edge launches, launch gaps,
     # the host merge and concurrent streams included (generic nonces, < 0.1%, not credited)

@@ -1,0 +1,77 @@
+"""loop_mix.py -- the issued instruction mix of every fast_search per-nonce loop (Makefile).
+
+    python3 loop_mix.py build/fast_search_prio.s build/fast_loop_mix.json
+
+The build changes the compiler's instruction stream (add3_split.py turns every third v_add3 into
+two full-rate adds), so the loop the GPU runs issues more instructions than the algorithm counts
+(plan.cpp nonce_cost) and fewer half-rate ones.  bench.py prices `frac` on the algorithm's count
+and takes the bound a build can reach from this file: for each fast_search<J, MODE>, the VALU
+instructions and the half-rate ones of its per-nonce loop, read from the assembly that is
+assembled into the embedded code object.  tools/isa_report.py prints the same loops.
+"""
+import json
+import re
+import sys
+
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from valu_rates import valu_rate  # noqa: E402  (the opcode tables of the issue-priority pass)
+
+
+def kernels(text):
+    """{mangled name: assembly body up to its s_endpgm} for every kernel of the file."""
+    out = {}
+    for m in re.finditer(r"^(_Z\S+):", text, flags=re.M):
+        end = text.find("s_endpgm", m.end())
+        out[m.group(1)] = text[m.end():end]
+    return out
+
+
+def inner_loop(body):
+    """Opcodes (VALU and s_setprio) of the loop block with the most VALU instructions: the
+    per-nonce body of fast_search (its innermost loop is the rare candidate scan)."""
+    lines = body.split("\n")
+    best = None
+    for i, l in enumerate(lines):
+        if "Loop Header" in l:
+            ins = []
+            for j in range(i, len(lines)):
+                s = lines[j].strip()
+                if s.startswith("v_") or s.startswith("s_setprio"):
+                    ins.append(s.split()[0])
+                if s.startswith("s_cbranch_scc") or s.startswith("s_branch"):
+                    break
+            if best is None or len(ins) > len(best):
+                best = ins
+    return best or []
+
+
+FAST = re.compile(r"^_ZN2mh11fast_searchILi(\d+)ELi(\d+)EE")
+
+
+def loop_mix(text):
+    """{"J,MODE": {"valu": N, "half": H}} of every fast_search kernel's per-nonce loop."""
+    out = {}
+    for name, body in kernels(text).items():
+        m = FAST.match(name)
+        if not m:
+            continue
+        ins = [x for x in inner_loop(body) if x != "s_setprio"]
+        out[f"{m.group(1)},{m.group(2)}"] = {"valu": len(ins),
+                                             "half": sum(1 for x in ins if valu_rate(x) == "H")}
+    return out
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    mix = loop_mix(open(src).read())
+    if len(mix) != 22 or any(v["valu"] == 0 for v in mix.values()):
+        sys.exit(f"loop_mix: expected 22 fast_search loops in {src}, found {len(mix)}")
+    with open(dst, "w") as f:
+        json.dump(mix, f, indent=0, sort_keys=True)
+    print(f"loop_mix: {len(mix)} per-nonce loops -> {dst}")
+
+
+if __name__ == "__main__":
+    main()

@@ -130,3 +130,23 @@ def test_kernel_clock_during_a_search(gpu):
     assert 1.0 < kc["ghz"] <= 2.5, kc
     assert len(kc["ghz_by_xcd"]) == 8 and kc["probes"] == 64, kc
     assert all(1.0 < g <= 2.5 for g in kc["ghz_by_xcd"].values()), kc
+
+
+def test_mix_bound_of_the_loop_as_built():
+    """The build splits every third add3 (csrc/add3_split.py), so the per-nonce loop issues more
+    instructions than nonce_ops and fewer half-rate ones; bench prices frac on nonce_ops and takes
+    the reachable bound from the built loop (build/fast_loop_mix.json).  At the fastest time that
+    loop allows, frac equals that bound, which is <= 1 and above the algorithm's own mix bound."""
+    mix = bench.fast_loop_mix()
+    assert mix is not None and len(mix) == 22
+    for cfg in ("2", "3a", "3b", "4"):
+        p = dominant_piece(cfg)
+        b = mix[(p["word"], p["mode"])]
+        alg_half = p["nonce_slots"] - p["nonce_ops"]
+        assert b["valu"] > p["nonce_ops"] and b["half"] < alg_half, (cfg, b)
+        quads = p["count"] / 64 * max(b["half"], b["valu"] / 2)
+        ns = quads * 4 / (CUS * 4 * bench.PEAK_SCLK_HZ) * 1e9
+        line = bench.roofline([kstat(p, ns)], CUS, 1, None, mix)
+        assert line["frac"] == pytest.approx(line["mix_bound_frac"], rel=2e-3)
+        assert line["alg_mix_bound_frac"] < line["mix_bound_frac"] <= 1.0
+        assert line["issued_loop"]["valu_per_nonce"] == b["valu"]

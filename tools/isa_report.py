@@ -18,15 +18,7 @@ import os  # noqa: E402
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "bitcoin-miner_amd", "csrc"))
 from valu_rates import HALF as HALF_RATE  # noqa: E402  (one table with the issue-priority pass)
-
-
-def kernels(text):
-    out = {}
-    for m in re.finditer(r"^(_Z\S+):", text, flags=re.M):
-        name = m.group(1)
-        end = text.find("s_endpgm", m.end())
-        out[name] = text[m.end():end]
-    return out
+from loop_mix import inner_loop, kernels  # noqa: E402  (the loop finder of the build's loop_mix.json)
 
 
 def meta(text):
@@ -39,25 +31,6 @@ def meta(text):
                 d[k] = int(mm.group(1))
         res[blk.group(1)] = d
     return res
-
-
-def inner_loop(body):
-    lines = body.split("\n")
-    best = None
-    for i, l in enumerate(lines):
-        # the per-nonce body is the loop block with the most VALU instructions (the
-        # innermost loop is the rare candidate scan of fast_search since r01zt)
-        if "Loop Header" in l:
-            ins = []
-            for j in range(i, len(lines)):
-                s = lines[j].strip()
-                if s.startswith("v_") or s.startswith("s_setprio"):
-                    ins.append(s.split()[0])
-                if s.startswith("s_cbranch_scc") or s.startswith("s_branch"):
-                    break
-            if best is None or len(ins) > len(best):
-                best = ins
-    return best or []
 
 
 def main():

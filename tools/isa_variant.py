@@ -108,7 +108,7 @@ def variant(name, base_text):
         # op, so the loop needs >= max(H, N/2) quad-cycles; trading some add3 (1 H) for two adds
         # (2 F) lowers H below N/2's growth (J = 4: H 701, N 1196).
         k = int(name[len("a3split"):])
-        t, n = split_add3(base_text, k)
+        t, n = add3_split.split(base_text, k)  # the build's own pass (per-kernel count)
         t2, n2 = prio_phases(t)
         return t2, n + n2
     if name.startswith("sched_"):
@@ -145,38 +145,11 @@ def variant(name, base_text):
 
 sys.path.insert(0, CSRC)
 from issue_prio import annotate, valu_class  # noqa: E402
+import add3_split  # noqa: E402
 
 
 def is_vgpr(op):
     return re.match(r"^v\d+$", op) is not None
-
-
-def split_add3(text, k):
-    out, n, i = [], 0, 0
-    for line, fast in in_fast(text):
-        m = re.match(r"^(\s+)v_add3_u32\s+(\S+),\s*(\S+),\s*(\S+),\s*(\S+)\s*$", line) if fast else None
-        if m:
-            i += 1
-            if i % k == 0:
-                ind, d, a, b, c = m.groups()
-                ops = [a, b, c]
-                # the operand added second must not be the destination (the first add overwrites it)
-                last = next((x for x in reversed(ops) if x != d), None)
-                if last is not None:
-                    ops.remove(last)
-                    x, y = ops
-                    if is_vgpr(y):
-                        first = f"{ind}v_add_u32_e32 {d}, {x}, {y}"
-                    elif is_vgpr(x):
-                        first = f"{ind}v_add_u32_e32 {d}, {y}, {x}"
-                    else:
-                        first = f"{ind}v_add_u32_e64 {d}, {x}, {y}"
-                    out.append(first)
-                    out.append(f"{ind}v_add_u32_e32 {d}, {last}, {d}")
-                    n += 1
-                    continue
-        out.append(line)
-    return "\n".join(out), n
 
 
 def prio_phases(text):

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--count", type=int, default=1 << 31)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--var", action="append", default=[], help="name:K=V,K=V")
+    ap.add_argument("--clock", action="store_true",
+                    help="also read each variant's in-kernel clock during a 2^37-nonce search of "
+                         "fast_search<4, One> (bench.kernel_clock; needs build/libclockprobe.so)")
     a = ap.parse_args()
     variants = []
     for v in a.var or ["base:"]:
@@ -67,6 +70,25 @@ def main():
                "wall_ghs_med": sorted(x["wall_ghs"] for x in v)[len(v) // 2],
                "wall_ghs_max": max(x["wall_ghs"] for x in v),
                "fast_ghs_max": max(x["fast_ghs"] for x in v), "result": v[-1]["result"]} for n, v in res.items()}
+    if a.clock:
+        sys.path.insert(0, ROOT)
+        import bench
+        for name, env in variants:
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            try:
+                kc = bench.kernel_clock(lambda m, lo, hi: minehip.search(m, lo, hi))
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            out[name]["kernel_clock"] = kc
+            if kc and kc.get("ghz"):
+                # SIMD quad-cycles per 64 nonces (one wave-iteration of the loop) in the probed search,
+                # at its own clock: 1,024 SIMDs, 4 cycles a quad; the <4, One> mix bound is 701
+                out[name]["simd_quads_per_64_nonces"] = round(kc["ghz"] / kc["search_ghs"] * 1024 * 64 / 4, 1)
     print(json.dumps(out))
 
 
