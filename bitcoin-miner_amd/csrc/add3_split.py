@@ -42,9 +42,15 @@ def split_line(m):
     return [first, f"{ind}v_add_u32_e32 {d}, {last}, {d}"]
 
 
-def split(text, k):
-    """Returns (text, add3 split).  k <= 0 leaves the text unchanged."""
-    if k <= 0:
+def split(text, k, pattern=None):
+    """Returns (text, add3 split).  Splits every k-th v_add3 of each fast kernel (k <= 0: none),
+    or, with `pattern` (a string of 0/1 repeated over each kernel's add3s, e.g. "001" = k 3),
+    those at a '1'."""
+    if pattern is None:
+        if k <= 0:
+            return text, 0
+        pattern = "0" * (k - 1) + "1"
+    if "1" not in pattern:
         return text, 0
     out, n, i, inside = [], 0, 0, False
     for line in text.split("\n"):
@@ -55,7 +61,7 @@ def split(text, k):
         m = ADD3.match(line) if inside else None
         if m:
             i += 1
-            if i % k == 0:
+            if pattern[(i - 1) % len(pattern)] == "1":
                 rep = split_line(m)
                 if rep is not None:
                     out.extend(rep)

@@ -102,6 +102,12 @@ def variant(name, base_text):
                 n += ch
             out.append(line)
         return "\n".join(out), n
+    if name.startswith("a3pat"):
+        # a3pat<pattern>: the add3 split at the '1's of a 0/1 pattern repeated over each fast
+        # kernel's add3s (a3pat001 = a3split3 = the build), then the issue-priority pass
+        t, n = add3_split.split(base_text, 0, pattern=name[len("a3pat"):])
+        t2, n2 = prio_phases(t)
+        return t2, n + n2
     if name.startswith("a3split"):
         # a3split<k>: every k-th v_add3_u32 of the fast kernels as two full-rate adds, then the
         # issue-priority pass.  A half-rate op cannot share its quad-cycle with another half-rate
