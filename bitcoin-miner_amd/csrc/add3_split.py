@@ -71,6 +71,58 @@ def split(text, k, pattern=None):
     return "\n".join(out), n
 
 
+def _reads(line, reg):
+    """Whether an instruction line reads register `reg` (any operand after the destination)."""
+    m = re.match(r"^\s+([sv]_\w+)\s+(.*)$", line)
+    if not m:
+        return False
+    ops = [o.strip() for o in m.group(2).split(",")]
+    return any(re.fullmatch(reg, o) for o in ops[1:])
+
+
+def split_by_slack(text, frac, horizon=400):
+    """Split the fraction `frac` of each fast kernel's add3s whose results are read latest: the
+    distance, in VALU instructions, from the add3 to the first instruction reading its destination
+    (two dependent adds take one more issue slot on that chain than one add3).  Returns (text, n)."""
+    lines = text.split("\n")
+    out, n = [], 0
+    i = 0
+    while i < len(lines):
+        if not re.match(r"^_ZN2mh11fast_search\S*:", lines[i]):
+            out.append(lines[i])
+            i += 1
+            continue
+        j = i
+        while j < len(lines) and not lines[j].startswith(".Lfunc_end"):
+            j += 1
+        body = lines[i:j]
+        cand = []
+        for a, ln in enumerate(body):
+            m = ADD3.match(ln)
+            if not m:
+                continue
+            d, dist = m.group(2), horizon
+            seen = 0
+            for b in range(a + 1, min(len(body), a + 1 + 4 * horizon)):
+                if body[b].strip().startswith("v_"):
+                    seen += 1
+                if _reads(body[b], re.escape(d)) or seen >= horizon:
+                    dist = seen
+                    break
+            cand.append((dist, a))
+        k = int(round(frac * len(cand)))
+        pick = {a for _, a in sorted(cand, key=lambda t: (-t[0], t[1]))[:k]}
+        for a, ln in enumerate(body):
+            rep = split_line(ADD3.match(ln)) if a in pick else None
+            if rep is not None:
+                out.extend(rep)
+                n += 1
+            else:
+                out.append(ln)
+        i = j
+    return "\n".join(out), n
+
+
 def main():
     k, src, dst = int(sys.argv[1]), sys.argv[2], sys.argv[3]
     text, n = split(open(src).read(), k)

@@ -85,3 +85,16 @@ def test_build_uses_the_split():
     """The Makefile runs the pass between the compiler's assembly and the issue-priority pass."""
     mk = open(os.path.join(os.path.dirname(PKG), "Makefile")).read()
     assert "add3_split.py" in mk
+
+
+def test_split_by_slack_picks_the_results_read_latest():
+    body = ["\tv_add3_u32 v1, v2, v3, v4",      # read by the very next instruction
+            "\tv_xor_b32_e32 v9, v1, v9",
+            "\tv_add3_u32 v5, v2, v3, v4"]     # read only after ten more instructions
+    body += [f"\tv_xor_b32_e32 v{10 + i}, v2, v3" for i in range(10)]
+    body += ["\tv_add_u32_e32 v6, v5, v6"]
+    asm = "_ZN2mh11fast_searchILi4ELi0EEEvNS_8FastArgsEPNS_7PartialE:\n" + "\n".join(body) + "\n.Lfunc_end0:\n"
+    out, n = add3_split.split_by_slack(asm, 0.5)
+    assert n == 1
+    assert "v_add3_u32 v1, v2, v3, v4" in out and "v_add3_u32 v5" not in out
+    assert add3_split.split_by_slack(asm, 0.0) == (asm, 0)

@@ -108,6 +108,11 @@ def variant(name, base_text):
         t, n = add3_split.split(base_text, 0, pattern=name[len("a3pat"):])
         t2, n2 = prio_phases(t)
         return t2, n + n2
+    if name.startswith("a3far"):
+        # a3far<pct>: split the pct% of each fast kernel's add3s whose results are read latest
+        t, n = add3_split.split_by_slack(base_text, int(name[len("a3far"):]) / 100)
+        t2, n2 = prio_phases(t)
+        return t2, n + n2
     if name.startswith("a3split"):
         # a3split<k>: every k-th v_add3_u32 of the fast kernels as two full-rate adds, then the
         # issue-priority pass.  A half-rate op cannot share its quad-cycle with another half-rate
