@@ -80,6 +80,7 @@ DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
     # (the s_barrier variants sync1/sync10 of round 2, -4%, profiles/r02k_kbench_sync.json, were removed
     # from the kernel source in round 3)
     "prio_w8": (["-DMH_MIN_WAVES=8"], True),   # <= 64 VGPRs: 8 waves/SIMD
+    "split_w8": (["-DMH_MIN_WAVES=8"], "split"),  # the same with the build's add3 split
     "prio_w6": (["-DMH_MIN_WAVES=6"], True),
     "prio_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], True),
     "prio_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], True),
@@ -241,6 +242,10 @@ def main():
             if prio in ("sched", "ub"):
                 from sched_pass import reorder
                 t, _ = reorder(open(s_path).read(), D=1, R=99, raw_only=(prio == "ub"))
+                t, n = prio_phases(t)
+                open(s_path, "w").write(t)
+            elif prio == "split":
+                t, _ = add3_split.split(open(s_path).read(), 3)
                 t, n = prio_phases(t)
                 open(s_path, "w").write(t)
             elif prio:
