@@ -23,10 +23,19 @@
 #include "layout.hpp"
 #include "sha256_gfx950.hpp"
 
-// minimum waves per SIMD the fast kernel is compiled for (register budget)
-#ifndef MH_MIN_WAVES
-#define MH_MIN_WAVES 1
+// Minimum waves per SIMD each fast_search<J, MODE> is compiled for (its register budget): the
+// occupancy the layout reaches as a one-chunk-per-workgroup kernel (VGPRs 59..79 -> 7 or 6 waves,
+// the Two layouts 98..110 -> 4).  The work-queue loop around the chunk body would otherwise let
+// the allocator take 4..6 more VGPRs and cost a wave per SIMD.  -DMH_MIN_WAVES=n overrides all.
+constexpr int min_waves(int J, int MODE) {
+#ifdef MH_MIN_WAVES
+    return MH_MIN_WAVES;
+#else
+    return MODE == 2 ? 4
+         : MODE == 1 ? ((J == 0 || J == 4) ? 6 : 7)
+                     : ((J == 7 || J == 8 || J >= 10) ? 6 : 7);
 #endif
+}
 
 namespace mh {
 
@@ -108,9 +117,10 @@ __device__ __forceinline__ void sha256_block_kw_last(const uint32_t st[8], const
 }
 }  // namespace dev
 
+// One workgroup-sized chunk: the 256 runs u_start + 256 * blk + threadIdx.x, their minimum
+// written to partials[blk].
 template <int J, int MODE>
-__global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const FastArgs a,
-                                                                           Partial* __restrict__ partials) {
+__device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restrict__ partials, const uint32_t blk) {
     using namespace dev;
     constexpr uint32_t K[64] = MH_K256;
     constexpr uint64_t NM = Dep::from(J);               // nonce-level words
@@ -119,7 +129,7 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
 #define MH_N(t) ((NM >> (t)) & 1ull)
 #define MH_G(t) ((GM >> (t)) & 1ull)
 #define MH_R(t) (!MH_N(t) && !MH_G(t))
-    const uint32_t gid = blockIdx.x * kBlockThreads + threadIdx.x;
+    const uint32_t gid = blk * kBlockThreads + threadIdx.x;
     const uint64_t U = a.u_start + gid;
 
     // ---- per run --------------------------------------------------------
@@ -198,7 +208,7 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
     // run.  Invalid lanes (gid >= n_runs) never become candidates.
     const uint64_t valid_mask = __builtin_amdgcn_ballot_w64(gid < a.n_runs);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t wave_u0 = a.u_start + (uint64_t)blockIdx.x * kBlockThreads + wave * 64u;
+    const uint64_t wave_u0 = a.u_start + (uint64_t)blk * kBlockThreads + wave * 64u;
     uint32_t wbh0 = 0xFFFFFFFFu, wbh1 = 0xFFFFFFFFu;
     uint64_t wbn = ~0ull;
 
@@ -320,7 +330,39 @@ __global__ __launch_bounds__(kBlockThreads, MH_MIN_WAVES) void fast_search(const
     uint64_t hash = ((uint64_t)wbh0 << 32) | wbh1;  // wave-uniform: the wave step of block_min
     uint64_t nonce = wbn;                            // is a no-op, the LDS step joins the waves
     block_min(hash, nonce);
-    if (threadIdx.x == 0) partials[blockIdx.x] = Partial{hash, nonce};
+    if (threadIdx.x == 0) partials[blk] = Partial{hash, nonce};
+}
+
+// The chunk the workgroup runs next: thread 0 takes it from the launch's counter (a vector
+// atomic, returning the old value), LDS hands it to the other waves.
+__device__ __forceinline__ uint32_t claim_chunk(uint32_t* counter) {
+    __shared__ uint32_t s_next;
+    if (threadIdx.x == 0) s_next = atomicAdd(counter, 1u);
+    __syncthreads();
+    const uint32_t blk = s_next;
+    __syncthreads();  // every wave has read it before thread 0 may overwrite it
+    return blk;
+}
+
+template <int J, int MODE>
+__global__ __launch_bounds__(kBlockThreads, min_waves(J, MODE)) void fast_search(const FastArgs a,
+                                                                           Partial* __restrict__ partials) {
+    // Static: workgroup b runs chunk b.  Work queue (a.counter set, grid <= the resident
+    // workgroups): each workgroup claims chunks until the counter passes n_chunks; every
+    // workgroup leaves once a claim comes back >= n_chunks, so the grid always drains.
+    // The chunk body reads its arguments through a pointer the loop launders every iteration,
+    // so the compiler cannot keep values derived from them live from one chunk to the next:
+    // hoisted out of the loop they spilled ~240 SGPRs into VGPR lanes (85 VGPRs instead of 70).
+    using KArgs = __attribute__((address_space(4))) const FastArgs;
+    KArgs* kp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t blk = a.counter ? claim_chunk(a.counter) : blockIdx.x;
+    while (blk < a.n_chunks) {
+        KArgs* k = kp;
+        asm volatile("" : "+s"(k));
+        fast_chunk<J, MODE>(*(const FastArgs*)k, partials, blk);
+        if (!a.counter) break;
+        blk = claim_chunk(a.counter);
+    }
 }
 
 // The instantiations the planner uses (plan.cpp; launch by mangled name in

@@ -43,8 +43,12 @@ struct FastArgs {
     uint32_t L;           // lower digits enumerated inside a lane (1..5)
     uint32_t n_groups;    // 10^(L-1): groups of 10 consecutive nonces per lane
     uint32_t mode;        // FastMode
-    uint32_t pad;
+    uint32_t n_chunks;    // workgroup-sized chunks (256 runs each) in this launch
     uint32_t kw1[64];     // kModeTwo: K[i] + W[i] of tail block 1 (padding + length only)
+    // Work queue: non-null -> the launch's workgroups claim chunks from this zeroed device
+    // counter until it passes n_chunks, so an XCD that clocks faster takes more of them;
+    // null -> workgroup b runs chunk b (grid = n_chunks).  DESIGN.md §3.
+    uint32_t* counter;
 };
 
 // Arguments of the generic per-nonce kernels (range edges, small buckets,

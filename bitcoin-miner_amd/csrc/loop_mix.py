@@ -28,23 +28,33 @@ def kernels(text):
     return out
 
 
-def inner_loop(body):
-    """Opcodes (VALU and s_setprio) of the loop block with the most VALU instructions: the
-    per-nonce body of fast_search (its innermost loop is the rare candidate scan)."""
+def loop_blocks(body):
+    """Opcodes of every loop-header block (up to its first scalar branch)."""
     lines = body.split("\n")
-    best = None
+    out = []
     for i, l in enumerate(lines):
         if "Loop Header" in l:
-            ins = []
+            ops = []
             for j in range(i, len(lines)):
                 s = lines[j].strip()
-                if s.startswith("v_") or s.startswith("s_setprio"):
-                    ins.append(s.split()[0])
+                if s and not s.startswith((";", ".")):
+                    ops.append(s.split()[0])
                 if s.startswith("s_cbranch_scc") or s.startswith("s_branch"):
                     break
-            if best is None or len(ins) > len(best):
-                best = ins
-    return best or []
+            out.append(ops)
+    return out
+
+
+def per_nonce_loop(body):
+    """All opcodes of the loop block with the most VALU instructions: the per-nonce body of
+    fast_search (its innermost loop is the rare candidate scan)."""
+    blocks = loop_blocks(body)
+    return max(blocks, key=lambda ops: sum(o.startswith("v_") for o in ops)) if blocks else []
+
+
+def inner_loop(body):
+    """Opcodes (VALU and s_setprio) of the per-nonce loop."""
+    return [o for o in per_nonce_loop(body) if o.startswith("v_") or o.startswith("s_setprio")]
 
 
 FAST = re.compile(r"^_ZN2mh11fast_searchILi(\d+)ELi(\d+)EE")
@@ -58,8 +68,10 @@ def loop_mix(text):
         if not m:
             continue
         ins = [x for x in inner_loop(body) if x != "s_setprio"]
-        out[f"{m.group(1)},{m.group(2)}"] = {"valu": len(ins),
-                                             "half": sum(1 for x in ins if valu_rate(x) == "H")}
+        out[f"{m.group(1)},{m.group(2)}"] = {
+            "valu": len(ins), "half": sum(1 for x in ins if valu_rate(x) == "H"),
+            # private-memory (spill) accesses inside the per-nonce loop: must stay 0
+            "loop_spill_ops": sum(1 for o in per_nonce_loop(body) if o.startswith(("scratch_", "buffer_")))}
     return out
 
 

@@ -27,8 +27,7 @@
 
 namespace mh {
 hipError_t fast_module_init(int dev);
-hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks,
-                       hipStream_t s);
+hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, hipStream_t s);
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
                              hipStream_t s);
@@ -62,6 +61,7 @@ namespace {
 
 constexpr uint64_t kBatchChunk = 1u << 22;  // nonces per hash_batch transfer
 constexpr int kEventPairs = 512;             // profiled launches buffered before harvesting
+constexpr uint32_t kQueueSlots = 4096;       // work-queue counters per search (one per fast launch)
 
 struct Timed {
     hipEvent_t start = nullptr, stop = nullptr;
@@ -89,6 +89,8 @@ struct DevCtx {
     uint64_t* d_nonces = nullptr;
     uint64_t* d_hashes = nullptr;
     uint32_t poff = 0;  // partials written since the last merge
+    uint32_t* d_counters = nullptr;  // work-queue counters, zeroed at each search's start
+    uint32_t qoff = 0;               // counters used by this search
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
@@ -143,6 +145,7 @@ int init_locked(DevCtx* c, int dev) {
         if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!c->d_partials) MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
     if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
+    if (!c->d_counters) MH_HIP(hipMalloc(&c->d_counters, sizeof(uint32_t) * kQueueSlots));
     if (!c->h_best) MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
     if (!c->d_nonces) MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
     if (!c->d_hashes) MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
@@ -218,6 +221,13 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     }
     Partial* out = c->d_partials + c->poff;
     Timed* tm = nullptr;
+    mh::FastArgs fa;
+    if (p.kind == 0) {
+        fa = p.fa;
+        fa.n_chunks = blocks;
+        // work queue while this search has counters left (a longer search runs the rest static)
+        fa.counter = (opt.queue && c->qoff < kQueueSlots) ? c->d_counters + c->qoff++ : nullptr;
+    }
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
@@ -232,7 +242,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
         MH_HIP(hipEventRecord(tm->start, s));
     }
     if (p.kind == 0)
-        MH_HIP(mh::launch_fast(c->dev, p.J, p.mode, p.fa, out, blocks, s));
+        MH_HIP(mh::launch_fast(c->dev, p.J, p.mode, fa, out, s));
     else
         MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, s));
     if (tm) MH_HIP(hipEventRecord(tm->stop, s));
@@ -266,6 +276,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //                          streams (default 2)
 //   MINEHIP_FINE_TAIL      nonces at the end of each full-L bucket planned at L - 1 (default
 //                          2^28; 0: none)
+//   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
+//                          XCDs take more; default); 0: one workgroup per chunk
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -287,6 +299,10 @@ mh::PlanOpts plan_opts() {
         if (v == 1 || v == 2) o.streams = v;
     }
     if (const char* e = getenv("MINEHIP_FINE_TAIL")) o.fine_tail = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("MINEHIP_QUEUE")) {
+        const int v = atoi(e);
+        if (v == 0 || v == 1) o.queue = v;
+    }
     return o;
 }
 
@@ -300,6 +316,8 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     MH_HIP(hipSetDevice(dev));
     MH_HIP(hipMemsetAsync(c->d_best, 0xFF, sizeof(Partial), c->stream));
     const mh::PlanOpts opt = plan_opts();
+    if (opt.queue) MH_HIP(hipMemsetAsync(c->d_counters, 0, sizeof(uint32_t) * kQueueSlots, c->stream));
+    c->qoff = 0;
     // Two streams only when there is something to overlap: coarse pieces and others.  A small
     // search (generic edges, short-lane buckets) stays on one stream and skips the events.  The
     // plan is streamed, never stored (a range can hold ~2^30 pieces); this first pass stops as

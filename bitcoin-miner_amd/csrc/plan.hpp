@@ -71,6 +71,12 @@ struct PlanOpts {
     // configs[3] shard +0.2%, and the predicted 8-GPU per-GPU efficiency 0.982 -> 1.00.
     int streams = 2;
     uint64_t fine_tail = 1ull << 28;
+    // Work queue (execution): a fast launch's workgroups claim 256-run chunks from a counter
+    // instead of one chunk each, so the 8 XCDs, whose clocks differ by a few percent, finish
+    // together.  Round 3, A/B in one process against one chunk per workgroup
+    // with the same code object: +0.6% to +1.9% on configs[1], configs[2]'s halves and the d = 10
+    // bucket (profiles/r03u_*).  0: one workgroup per chunk.
+    int queue = 1;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

@@ -19,6 +19,8 @@
 // Every candidate comparison is the lexicographic (hash, nonce) order, which
 // equals the reference loop's strict-< first minimum.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -208,8 +210,30 @@ hipError_t fast_module_init(int dev) {
     return fast_function(dev, 4, kModeOne, &f);
 }
 
-hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, uint32_t blocks,
-                       hipStream_t s) {
+// Workgroups of f that fit on dev at once (occupancy x CUs), cached per function.
+hipError_t resident_groups(int dev, hipFunction_t f, unsigned lds, uint32_t* out) {
+    static std::mutex mu;
+    static std::map<std::pair<hipFunction_t, unsigned>, uint32_t> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find({f, lds});
+    if (it == cache.end()) {
+        int per_cu = 0, cus = 0;
+        hipError_t e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kBlockThreads, lds);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return e;
+        }
+        it = cache.emplace(std::make_pair(f, lds), (uint32_t)std::max(1, per_cu) * (uint32_t)std::max(1, cus)).first;
+    }
+    *out = it->second;
+    return hipSuccess;
+}
+
+// a.n_chunks chunks of 256 runs; static (a.counter null): one workgroup per chunk; work queue:
+// as many workgroups as fit at once (an over-estimate only queues some of them), each claiming
+// chunks from a.counter (zeroed by the caller, one counter per launch).
+hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, hipStream_t s) {
     if (!fast_variant_exists(J, mode)) return hipErrorInvalidValue;
 #ifdef MH_DEV_HOOKS
     // MINEHIP_DEV_LDS (dev build only): reserve dynamic LDS per workgroup to
@@ -222,12 +246,19 @@ hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* par
     constexpr unsigned lds = 0;
 #endif
     hipFunction_t f;
-    const hipError_t e = fast_function(dev, J, mode, &f);
+    hipError_t e = fast_function(dev, J, mode, &f);
     if (e != hipSuccess) return e;
+    uint32_t grid = a.n_chunks;
+    if (a.counter) {
+        uint32_t resident = 0;
+        e = resident_groups(dev, f, lds, &resident);
+        if (e != hipSuccess) return e;
+        grid = std::min(grid, resident);
+    }
     FastArgs args = a;
     Partial* out = partials;
     void* params[] = {&args, &out};
-    return hipModuleLaunchKernel(f, blocks, 1, 1, kBlockThreads, 1, 1, lds, s, params, nullptr);
+    return hipModuleLaunchKernel(f, grid, 1, 1, kBlockThreads, 1, 1, lds, s, params, nullptr);
 }
 
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s) {

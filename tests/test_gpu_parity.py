@@ -170,14 +170,19 @@ def test_plan_invariance_small(gpu):
         for Ld in (1, 2, 3, 4, 5):
             for gb in (0, 1 << 20):
                 for st, ft in ((1, 0), (2, 0), (2, 20_000), (1, 99_999)):
-                    with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
-                             MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft):
-                        assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st, ft)
-        # tiny grids: many launches per bucket and many partial-buffer flushes (on both streams)
+                    for q in (0, 1):  # one workgroup per chunk / work queue
+                        with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
+                                 MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
+                                 MINEHIP_QUEUE=q):
+                            assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st, ft, q)
+        # tiny grids: many launches per bucket and many partial-buffer flushes (on both streams);
+        # with one block per launch a search outruns the 4,096 work-queue counters, and the
+        # launches past them run one workgroup per chunk
         for mb in (1, 3, 1000):
             for st in (1, 2):
-                with env(MINEHIP_MAX_BLOCKS=mb, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st):
-                    assert gpu.search(m, lo, hi) == exp, (m[:8], mb, st)
+                for q in (0, 1):
+                    with env(MINEHIP_MAX_BLOCKS=mb, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st, MINEHIP_QUEUE=q):
+                        assert gpu.search(m, lo, hi) == exp, (m[:8], mb, st, q)
 
 
 @pytest.mark.parametrize("msg,bits", [(b"cmu440", 32), (b"a" * 100, 34), (b"x" * 60, 34)])
