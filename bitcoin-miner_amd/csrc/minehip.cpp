@@ -221,9 +221,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     }
     Partial* out = c->d_partials + c->poff;
     Timed* tm = nullptr;
-    mh::FastArgs fa;
+    mh::FastArgs fa = p.fa;
     if (p.kind == 0) {
-        fa = p.fa;
         fa.n_chunks = blocks;
         // work queue while this search has counters left (a longer search runs the rest static)
         fa.counter = (opt.queue && c->qoff < kQueueSlots) ? c->d_counters + c->qoff++ : nullptr;
