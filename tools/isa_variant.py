@@ -81,6 +81,7 @@ DEFINES = {  # name: (extra compiler flags, apply the issue-priority pass)
     # from the kernel source in round 3)
     "prio_w8": (["-DMH_MIN_WAVES=8"], True),   # <= 64 VGPRs: 8 waves/SIMD
     "split_w8": (["-DMH_MIN_WAVES=8"], "split"),  # the same with the build's add3 split
+    "split_w1": (["-DMH_MIN_WAVES=1"], "split"),  # no register cap: the allocator's own choice
     "prio_w6": (["-DMH_MIN_WAVES=6"], True),
     "prio_ilp": (["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"], True),
     "prio_maxilp": (["-mllvm", "--amdgpu-sched-strategy=max-ilp"], True),
