@@ -153,3 +153,18 @@ def test_mix_bound_of_the_loop_as_built():
         assert line["frac"] == pytest.approx(line["mix_bound_frac"], rel=2e-3)
         assert line["alg_mix_bound_frac"] < line["mix_bound_frac"] <= 1.0
         assert line["issued_loop"]["valu_per_nonce"] == b["valu"]
+
+
+def test_fast_kernel_arguments_start_at_the_kernarg_segment():
+    """fast_search's work-queue loop re-reads FastArgs through __builtin_amdgcn_kernarg_segment_ptr()
+    (fast_search.hip), which assumes the by-value FastArgs is the first explicit argument at
+    offset 0 and the partials pointer follows it.  Checked on every kernel of the embedded code
+    object's metadata."""
+    kernels = [k for k in codeobj.metadata(codeobj.fast_code_object())["amdhsa.kernels"]
+               if k[".name"].startswith("_ZN2mh11fast_search")]
+    assert len(kernels) == 22
+    for k in kernels:
+        args = [a for a in k[".args"] if not a[".value_kind"].startswith("hidden_")]
+        assert [a[".offset"] for a in args] == [0, args[0][".size"]], k[".name"]
+        assert args[0][".value_kind"] == "by_value" and args[1][".value_kind"] == "global_buffer"
+        assert args[0][".size"] % 8 == 0 and args[1][".size"] == 8
