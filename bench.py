@@ -841,6 +841,11 @@ def main():
             # this VALU-bound kernel at its package power limit, so the clock, and with it value,
             # differs from box to box
             "sclk_ghz": roof.get("sclk_ghz"),
+            # the clock read inside the GPU during an un-profiled search of the dominant kernel (N = 1),
+            # and value per GHz of it: the box-independent rate (boxes differ by their clock, §4)
+            "kernel_clock_ghz": (roof.get("kernel_clock") or {}).get("ghz"),
+            "ghs_per_kernel_ghz": (round(value / roof["kernel_clock"]["ghz"], 3)
+                                   if (roof.get("kernel_clock") or {}).get("ghz") else None),
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,
