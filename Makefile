@@ -30,7 +30,7 @@ RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
 DEVLIB  := $(BUILD)/dev/libminehip.so
 
-all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so $(FAST_MIX)
+all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so $(FAST_MIX) $(BUILD)/fast_search_nomarker.hsaco
 
 # LSP endpoint (host only, wire compatible with the reference's Go lsp package)
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
@@ -53,7 +53,14 @@ $(DEVLIB): $(SRCS) $(HDRS) $(FAST_O)
 $(FAST_S): $(CSRC)/fast_search.hip $(FAST_HDRS)
 	mkdir -p $(BUILD)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $(FASTFLAGS) --cuda-device-only -S -o $@ $<
-$(FAST_SP): $(FAST_S) $(CSRC)/add3_split.py
+# the split factor is a prerequisite: `make ADD3_SPLIT=k` after a build redoes the split (and the
+# loop mix bench.py reads) instead of reusing the old assembly
+ADD3_STAMP := $(BUILD)/add3_split.$(ADD3_SPLIT).stamp
+$(ADD3_STAMP):
+	mkdir -p $(BUILD)
+	rm -f $(BUILD)/add3_split.*.stamp
+	touch $@
+$(FAST_SP): $(FAST_S) $(CSRC)/add3_split.py $(ADD3_STAMP)
 	python3 $(CSRC)/add3_split.py $(ADD3_SPLIT) $< $@
 $(FAST_PS): $(FAST_SP) $(CSRC)/issue_prio.py $(CSRC)/valu_rates.py
 	python3 $(CSRC)/issue_prio.py $< $@
@@ -62,6 +69,13 @@ $(FAST_MIX): $(FAST_PS) $(CSRC)/loop_mix.py $(CSRC)/valu_rates.py
 $(FAST_CO): $(FAST_PS)
 	$(LLVM)/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c -o $(BUILD)/fast_search_prio.o $<
 	$(LLVM)/ld.lld -shared -o $@ $(BUILD)/fast_search_prio.o
+# test artefact: the same kernels without the work-queue marker (mh_fast_queue_args), as a code
+# object built from older sources would be; the dev build must run it one workgroup per chunk
+# (tests/test_gpu_parity.py::test_code_object_without_queue_marker_runs_static)
+$(BUILD)/fast_search_nomarker.hsaco: $(FAST_PS)
+	grep -v mh_fast_queue_args $< > $(BUILD)/fast_search_nomarker.s
+	$(LLVM)/clang -x assembler -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c -o $(BUILD)/fast_search_nomarker.o $(BUILD)/fast_search_nomarker.s
+	$(LLVM)/ld.lld -shared -o $@ $(BUILD)/fast_search_nomarker.o
 $(FAST_O): $(CSRC)/fast_co.S $(FAST_CO)
 	gcc -c -fPIC -Wa,-I,$(BUILD) -o $@ $<
 
@@ -107,7 +121,9 @@ build/valu_%: tools/valu_%.hip
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 
 clean:
-	rm -f $(LIB) $(DEVLIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_PS) $(FAST_CO) $(FAST_O) $(BUILD)/fast_search_prio.o
+	rm -f $(LIB) $(DEVLIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_SP) $(FAST_PS) $(FAST_MIX) $(FAST_CO) $(FAST_O) \
+	      $(BUILD)/fast_search_prio.o $(BUILD)/libclockprobe.so $(BUILD)/add3_split.*.stamp \
+	      $(BUILD)/fast_search_nomarker.*
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle asm clean probes dev

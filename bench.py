@@ -24,10 +24,13 @@ shard, merged on the host):
     mh_search; the tuples, the barrier and the max-over-ranks time go over a
     gloo (host) process group.  WORLD_SIZE must equal --gpus.
   * self-contained (`python bench.py --gpus N`, no launcher): one process, one
-    host thread + HIP stream per device, mh_search_multi over devices 0..N-1
-    (the library's scheduler hands out chunks sized to each device's rate and
-    merges on the host).  Fewer than N visible devices is an error: exit 2, no
-    JSON line.  `--multi` forces this path at N = 1.
+    host thread + HIP stream per device, mh_search_multi over devices 0..N-1:
+    each step is one contiguous shard per device, sized by the device's rate
+    measured on the earlier steps (the library keeps the rates), merged on the
+    host.  Fewer than N visible devices is an error: exit 2, no JSON line.
+    `--multi` forces this path at N = 1.
+Every line carries `n1_config4_ghs`, one configs[3] step searched on one device
+alone, and configs[3] lines `per_gpu_efficiency` = value / (N x it).
 
 Rank 0 prints ONE JSON line.  `roofline.frac` is the dominant kernel's
 algorithmic per-nonce work (nonce_ops: the VALU instructions one nonce needs
@@ -268,6 +271,41 @@ def cpu_model():
     return "unknown"
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup quota allows this process (cgroup v2 cpu.max, v1 cfs files), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // p)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_threads():
+    """Threads for the CPU baseline and how they were chosen.  Every core this process may run on
+    (its affinity mask), capped by a cgroup CPU quota and by the job's CPU share: the GPU box
+    exports OMP_NUM_THREADS as each one-GPU job's share of a much larger machine (its affinity
+    shows every core of the node), and a job must not run more threads than that.
+    BENCH_CPU_THREADS overrides.  Returns (threads, facts for the line)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    facts = {"cores_available": avail, "cgroup_quota_cores": quota, "job_cpu_share": share}
+    if os.environ.get("BENCH_CPU_THREADS"):
+        facts["cores_rule"] = "BENCH_CPU_THREADS"
+        return max(1, int(os.environ["BENCH_CPU_THREADS"])), facts
+    t = min(x for x in (avail, quota, share) if x)
+    facts["cores_rule"] = ("min(affinity cores, cgroup quota, the job's CPU share OMP_NUM_THREADS)"
+                           if t < avail else "every core in the affinity mask")
+    return t, facts
+
+
 def cpu_baseline(msg, threads):
     """The reference loop ported to C (oracle/): per nonce format "%s %d" and a
     full SHA-256 from the IV, like bitcoin/hash.go.  Bounded sample of the
@@ -466,6 +504,31 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
                     "fast_search<4, One> (tools/clock_probe.hip)"}
 
 
+def same_workload_n1(search_dev, steps):
+    """One step of the scaling workload on ONE device: BASELINE configs[3]'s middle slice
+    ("cmu440", 2^40 / K nonces with K = max(steps, 20): the driver's --steps 20 step) searched
+    alone.  The N > 1 lines run configs[3] and the N = 1 line configs[1], so the driver's 1 -> N
+    ratio would otherwise compare two workloads; every line carries this N = 1 figure of the same
+    work (`n1_config4_ghs`) and, for configs[3] lines, value / (N x it) (`per_gpu_efficiency`)."""
+    cfg = CONFIGS["4"]
+    k_all = max(steps, 20)
+    k = k_all // 2
+    lo, hi = step_range(cfg, k, k_all)
+    msg = cfg["msg"].encode()
+    search_dev(msg, lo, lo + (1 << 30) - 1)  # untimed: device context, module and clocks up
+    t = time.perf_counter()
+    r = search_dev(msg, lo, hi)
+    dt = time.perf_counter() - t
+    return {"ghs": round((hi - lo + 1) / dt / 1e9, 4), "ms": round(dt * 1e3, 3), "range": [lo, hi],
+            "slice": f"step {k} of {k_all}", "result": list(r),
+            "golden_ok": None if golden_expect(msg, lo, hi) is None else tuple(r) == golden_expect(msg, lo, hi)}
+
+
+def per_gpu_efficiency(value, n_gpus, n1_ghs):
+    """A line's whole-job GH/s over N x the one-device GH/s of the same workload."""
+    return round(value / (n_gpus * n1_ghs), 4)
+
+
 def power_sample(search_dev, dev=0, seconds=1.0):
     """amd-smi's socket power and GFX clocks sampled once while a ~1.5 s search runs (N = 1,
     after the timed region).  The kernel is VALU-bound at the package power limit, so power
@@ -640,6 +703,8 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--no-clock", action="store_true",
                     help="skip the in-kernel clock probe after the timed region (tools/clock_probe.hip)")
+    ap.add_argument("--no-n1", action="store_true",
+                    help="skip the one-device search of a configs[3] step (n1_config4_ghs)")
     args = ap.parse_args()
     if args.gpus < 1 or args.steps < 1 or args.warmup < 0:
         die("--gpus and --steps must be >= 1, --warmup >= 0")
@@ -711,6 +776,12 @@ def main():
     barrier = (lambda: dist.barrier()) if launched else (lambda: None)
     for w in range(args.warmup):
         step(w)
+    n1 = None
+    if n_gpus > 1 and not args.no_n1:
+        # the same workload on device 0 alone, before the timed region (the other ranks wait)
+        if rank == 0:
+            n1 = same_workload_n1(lambda m, a, b: minehip.search(m, a, b, devs[0]), steps)
+        barrier()
     for d in uniq:
         minehip.profile_enable(d, True)
     r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize)
@@ -750,6 +821,17 @@ def main():
     kst = kernel_totals([p["kstats"] for p in per_dev])
     from minehip import codeobj
     roof = roofline(kst, cus, len(per_dev), codeobj.fast_kernel_resources(), fast_loop_mix())
+    streams = 1 if os.environ.get("MINEHIP_STREAMS") == "1" else 2  # PlanOpts.streams (minehip.cpp plan_opts)
+    roof["timing"] = {
+        "source": "HIP events recorded around each fast launch on the stream it runs on (mh_profile_*)",
+        "streams": streams,
+        # with two streams an event span is a wall span: it includes any wait for CUs the other
+        # stream's workgroups hold
+        "wall_span": streams == 2,
+        "note": "the dominant (full-L) launches go out first on the high-priority stream, so their spans "
+                "are close to kernel time; tools/trace_frac.py recomputes frac from the rocprofv3 trace "
+                "of the same command (per (kernel, queue) rows: profiles/*_kernel_stats_by_queue.csv)"
+                if streams == 2 else "one stream: launches run one after another, spans are kernel times"}
     # the whole timed region on the same basis: every fast piece's nonces x nonce_ops over the
     # max-over-ranks wall time and all N GPUs' peak -- tails, generic edge launches, launch gaps,
     # the host merge and concurrent streams included (generic nonces, < 0.1%, not credited)
@@ -798,10 +880,15 @@ def main():
         m_lo = job_range(cfg, n_gpus, 0, steps)[0]
         m_hi = job_range(cfg, n_gpus, steps - 1, steps)[1]
         expect = golden_expect(msg, m_lo, m_hi)
+        if n_gpus == 1 and not args.no_n1:
+            n1 = same_workload_n1(lambda m, a, b: minehip.search(m, a, b, devs[0]), steps)
         cpu = None
         if n_gpus == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            threads, facts = cpu_threads()
             cpu = cpu_baseline(cfg["msg"], threads)
+            cpu.update(facts)
+            # the shipped single-goroutine loop scales per core: what every visible core would do
+            cpu["all_cores_estimate_ghs"] = round(cpu["single_thread_value"] * facts["cores_available"], 6)
             cpu["gpu_config1"] = gpu_config1(lambda m, a, b: minehip.search(m, a, b, devs[0]))
         if n_gpus == 1 and not launched and not args.no_pmc:
             roof["power"] = power_sample(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
@@ -829,6 +916,9 @@ def main():
                        if p["kstats"] and p["kstats"][0]["ns"] else None,
                        "kernel_clock_ghz": p.get("kernel_clock_ghz")}
                       for p in per_dev]
+        if multi:  # the rates the library sized the last step's shards by (cost units per ns)
+            for pd, r in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
+                pd["multi_rate"] = round(r, 1)
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -846,6 +936,12 @@ def main():
             "kernel_clock_ghz": (roof.get("kernel_clock") or {}).get("ghz"),
             "ghs_per_kernel_ghz": (round(value / roof["kernel_clock"]["ghz"], 3)
                                    if (roof.get("kernel_clock") or {}).get("ghz") else None),
+            # the scaling workload on one device (same_workload_n1): the N = 1 point of a configs[3]
+            # curve, and this line's value against N times it when the line runs configs[3]
+            "n1_config4_ghs": n1["ghs"] if n1 else None,
+            "per_gpu_efficiency": (per_gpu_efficiency(value, n_gpus, n1["ghs"])
+                                   if n1 and cfg_name == "4" and args.bits is None and args.msg is None else None),
+            "n1_config4": n1,
             "higher_is_better": True,
             "scaling": cfg["scaling"],
             "vs_baseline": None,
@@ -864,7 +960,8 @@ def main():
                 "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
                 "shards": ("each strong step split in proportion to every rank's measured search rate "
                            "(gathered with the step's merge)" if launched and bal.enabled else
-                           "scheduler chunks sized to each device's rate" if multi else "equal"),
+                           "one shard per device per step, sized by each device's rate measured on the earlier "
+                           "steps (mh_search_multi)" if multi else "equal"),
             },
             "per_device": per_device,
             "roofline": roof,

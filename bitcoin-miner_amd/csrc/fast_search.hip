@@ -365,6 +365,15 @@ __global__ __launch_bounds__(kBlockThreads, min_waves(J, MODE)) void fast_search
     }
 }
 
+// Marker of a code object whose fast_search kernels run the work-queue loop above over this
+// FastArgs layout: its size is sizeof(FastArgs).  The library uses the work queue with a code
+// object only if it carries the marker at that size (search_kernels.hip, fast_function) -- the
+// embedded object always does; one loaded by the dev build's MINEHIP_DEV_CODE_OBJECT hook from
+// older sources runs one workgroup per chunk instead of searching only its first chunks.
+extern "C" {
+__device__ __attribute__((used)) uint8_t mh_fast_queue_args[sizeof(FastArgs)];
+}
+
 // The instantiations the planner uses (plan.cpp; launch by mangled name in
 // search_kernels.hip): kModeOne for every word J of the last digit in a
 // one-block tail, kModePre for J <= 4 of block 1 (last digit at tail byte

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 
 namespace mh {
 namespace {
@@ -216,7 +217,97 @@ bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, 
     return true;
 }
 
+// The fast layout of bucket d's nonces [A, B] (A <= B, all of [lower, upper] that lies in the
+// bucket): L as the planner picks it, or false when the bucket goes to the generic kernel.
+bool bucket_layout(const Prefix& pre, int d, uint64_t A, uint64_t B, const PlanOpts& opt, int* L_out, int* J,
+                   int* mode, int* nb, FastArgs* fa) {
+    int L = std::min(opt.lower_digits, d - 1);
+    L = std::min(L, 5);
+    // A lane runs 10^L nonces serially: a bucket with few runs would leave
+    // most SIMDs idle and end in a long tail, so shorten the runs until
+    // the bucket has min_lanes of them (2^21: ~8 workgroups per CU).
+    while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
+    while (L >= 1 && !make_fast_args(pre, d, L, J, mode, nb, fa)) --L;
+    *L_out = L;
+    return L >= 1 && B - A >= opt.generic_below;
+}
+
+inline uint64_t bucket_lo(int d) { return d == 1 ? 0u : kPow10[d - 1]; }
+inline uint64_t bucket_hi(int d) { return d == 20 ? ~(uint64_t)0 : kPow10[d] - 1u; }
+
 }  // namespace
+
+void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
+                   std::vector<CostSeg>* out) {
+    out->clear();
+    const int d_lo = decimal_digits(lower), d_hi = decimal_digits(upper);
+    for (int d = d_lo; d <= d_hi; ++d) {
+        const uint64_t A = std::max(lower, bucket_lo(d)), B = std::min(upper, bucket_hi(d));
+        int L = 0, J = 0, mode = 0, nb = 1;
+        FastArgs fa;
+        double per;
+        if (bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &fa)) {
+            // the fast kernel's issue slots per nonce, plus the per-run / per-group work that shorter
+            // lanes amortise over fewer nonces (L = 2: ~3%, L = 1: ~6% per nonce)
+            per = (double)nonce_cost(J, mode).slots * (1.0 + 0.03 * (double)(3 - std::min(L, 3)));
+        } else {
+            // generic kernel: every nonce formatted and hashed from the midstate
+            const int blocks = (pre.t + (uint32_t)d + 9u <= 64u) ? 1 : 2;
+            per = (double)kGenericSlotsPerBlock * blocks;
+        }
+        out->push_back(CostSeg{A, B, per});
+    }
+}
+
+double segments_cost(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi) {
+    double c = 0.0;
+    for (const CostSeg& s : segs) {
+        const uint64_t a = std::max(s.a, lo), b = std::min(s.b, hi);
+        if (a <= b) c += ((double)(b - a) + 1.0) * s.per;
+    }
+    return c;
+}
+
+void split_by_cost(const std::vector<CostSeg>& segs, const std::vector<double>& w, std::vector<Span>* out) {
+    out->assign(w.size(), Span{0, 0, true});
+    if (segs.empty() || w.empty()) return;
+    using u128 = unsigned __int128;
+    double wsum = 0.0;
+    for (double x : w) wsum += std::max(0.0, x);
+    double total = 0.0;
+    for (const CostSeg& s : segs) total += ((double)(s.b - s.a) + 1.0) * s.per;
+    const uint64_t lower = segs.front().a;
+    const u128 n_all = (u128)(segs.back().b - lower) + 1u;
+    // Cut k (k = 1..n-1) after the nonce where the cost so far reaches total x (w_0 + .. + w_{k-1}) /
+    // wsum; positions are nonce counts from lower (integers, monotone, the last one n_all), so the
+    // spans tile [lower, upper] exactly whatever the rounding of the costs.
+    u128 prev = 0;
+    double acc_w = 0.0;
+    for (size_t k = 0; k < w.size(); ++k) {
+        acc_w += std::max(0.0, w[k]);
+        u128 pos;
+        if (k + 1 == w.size() || wsum <= 0.0) {
+            pos = (k + 1 == w.size()) ? n_all : prev;
+        } else {
+            double target = total * (acc_w / wsum), cum = 0.0;
+            pos = n_all;
+            for (const CostSeg& s : segs) {
+                const double len = (double)(s.b - s.a) + 1.0, c = len * s.per;
+                if (cum + c >= target) {
+                    double n = std::floor((target - cum) / s.per);
+                    n = std::min(std::max(n, 0.0), len);
+                    pos = (u128)(s.a - lower) + (u128)n;
+                    break;
+                }
+                cum += c;
+            }
+            if (pos > n_all) pos = n_all;
+        }
+        if (pos < prev) pos = prev;
+        if (pos > prev) (*out)[k] = Span{(uint64_t)(lower + (prev)), (uint64_t)(lower + (pos - 1u)), false};
+        prev = pos;
+    }
+}
 
 void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
                  const std::function<bool(const Piece&)>& cb) {
@@ -268,18 +359,10 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
     };
 
     for (int d = d_lo; d <= d_hi; ++d) {
-        const uint64_t A = std::max<uint64_t>(lower, d == 1 ? 0u : kPow10[d - 1]);
-        const uint64_t B = std::min<uint64_t>(upper, d == 20 ? ~(uint64_t)0 : kPow10[d] - 1u);
-        int L = std::min(opt.lower_digits, d - 1);
-        L = std::min(L, 5);
-        // A lane runs 10^L nonces serially: a bucket with few runs would leave
-        // most SIMDs idle and end in a long tail, so shorten the runs until
-        // the bucket has min_lanes of them (2^21: ~8 workgroups per CU).
-        while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
+        const uint64_t A = std::max(lower, bucket_lo(d)), B = std::min(upper, bucket_hi(d));
         FastArgs fa;
-        int J = 0, mode = 0, nb = 1;
-        while (L >= 1 && !make_fast_args(pre, d, L, &J, &mode, &nb, &fa)) --L;
-        if (L < 1 || B - A < opt.generic_below) {
+        int L = 0, J = 0, mode = 0, nb = 1;
+        if (!bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &fa)) {
             if (!emit_generic(A, B, d)) return;
             continue;
         }

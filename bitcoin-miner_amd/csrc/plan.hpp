@@ -10,6 +10,7 @@
 #include <stddef.h>
 
 #include <functional>
+#include <vector>
 
 #include "layout.hpp"
 
@@ -103,5 +104,29 @@ struct NonceCost {
 NonceCost nonce_cost(int J, int mode);
 
 int decimal_digits(uint64_t n);
+
+// ---- relative search cost, for splitting a range over devices (mh_search_multi) ----
+// One segment per decimal bucket of [lower, upper]: every nonce of [a, b] costs `per` issue slots
+// -- the fast kernel's nonce_cost slots at the bucket's planned L (shorter lanes a few percent
+// more), or kGenericSlotsPerBlock per tail block for a bucket the planner gives the generic
+// kernel.  A device's rate in these units (slots per ns) does not depend on which layouts its
+// range happened to hold, so rates measured on one range size the shards of the next.
+struct CostSeg {
+    uint64_t a, b;  // inclusive
+    double per;
+};
+constexpr double kGenericSlotsPerBlock = 4.0 * 1760.0;  // formatting + a full compression, scalar-ish
+void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
+                   std::vector<CostSeg>* out);
+double segments_cost(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi);
+
+struct Span {
+    uint64_t lo, hi;  // inclusive
+    bool empty;
+};
+// Cut the segments' range into w.size() contiguous spans in order, span k carrying a share of the
+// total cost proportional to w[k] (>= 0).  The spans tile the range exactly (integer cut
+// positions); a span whose share rounds to no nonce is empty.
+void split_by_cost(const std::vector<CostSeg>& segs, const std::vector<double>& w, std::vector<Span>* out);
 
 }  // namespace mh

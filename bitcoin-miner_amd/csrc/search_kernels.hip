@@ -158,8 +158,11 @@ namespace {
 std::mutex g_mod_mu;
 std::map<std::pair<std::string, int>, hipModule_t> g_mods;                    // (file or "", dev)
 std::map<std::pair<hipModule_t, int>, hipFunction_t> g_funcs;                // (module, J + 16 * mode)
+std::map<hipModule_t, bool> g_queue_ok;  // the module's kernels run the work-queue loop (marker)
 
-hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f) {
+// queue_ok: the code object carries fast_search.hip's mh_fast_queue_args marker at this
+// library's sizeof(FastArgs), i.e. its kernels claim chunks from a.counter
+hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f, bool* queue_ok = nullptr) {
 #ifdef MH_DEV_HOOKS
     const char* co = getenv("MINEHIP_DEV_CODE_OBJECT");
     const std::string path = (co && *co) ? co : "";
@@ -176,7 +179,14 @@ hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f) {
             return e;
         }
         it = g_mods.emplace(std::make_pair(path, dev), m).first;
+        hipDeviceptr_t gp = nullptr;
+        size_t gsz = 0;
+        const bool marked = hipModuleGetGlobal(&gp, &gsz, m, "mh_fast_queue_args") == hipSuccess &&
+                            gsz == sizeof(FastArgs);
+        (void)hipGetLastError();
+        g_queue_ok[m] = marked;
     }
+    if (queue_ok) *queue_ok = g_queue_ok[it->second];
     auto fit = g_funcs.find({it->second, J + 16 * mode});
     if (fit == g_funcs.end()) {
         char name[96];
@@ -246,16 +256,18 @@ hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* par
     constexpr unsigned lds = 0;
 #endif
     hipFunction_t f;
-    hipError_t e = fast_function(dev, J, mode, &f);
+    bool queue_ok = false;
+    hipError_t e = fast_function(dev, J, mode, &f, &queue_ok);
     if (e != hipSuccess) return e;
     uint32_t grid = a.n_chunks;
-    if (a.counter) {
+    FastArgs args = a;
+    if (!queue_ok) args.counter = nullptr;  // a code object without the loop: one workgroup per chunk
+    if (args.counter) {
         uint32_t resident = 0;
         e = resident_groups(dev, f, lds, &resident);
         if (e != hipSuccess) return e;
         grid = std::min(grid, resident);
     }
-    FastArgs args = a;
     Partial* out = partials;
     void* params[] = {&args, &out};
     return hipModuleLaunchKernel(f, grid, 1, 1, kBlockThreads, 1, 1, lds, s, params, nullptr);

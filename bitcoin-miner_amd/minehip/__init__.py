@@ -17,7 +17,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import lib, mh_piece, mh_message, mh_kernel_stat, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
+from ._lib import lib, mh_piece, mh_message, mh_kernel_stat, mh_span, OPS_PER_BLOCK, EXPORTS, LIB_PATH  # noqa: F401
 from ._lib import MH_OK, MH_EINVAL, MH_ERANGE, MH_ETOOLONG, MH_ENODEV, MH_EHIP  # noqa: F401
 from ._lib import MH_ENOTREQ, MH_EINTERNAL, MH_EREJECTED  # noqa: F401
 
@@ -87,6 +87,28 @@ def plan(msg, lower, upper, cap=1 << 16):
     if k > cap:
         raise ValueError("plan longer than cap")
     return [{f: getattr(buf[i], f) for f, _ in mh_piece._fields_} for i in range(k)]
+
+
+def multi_plan(msg, lower, upper, ndev, weights=None, cap=1 << 12):
+    """Host-only: how search_multi (chunk = 0) splits [lower, upper] over ndev workers with rates in
+    proportion to `weights` (None = equal): head shards, then tail chunks (list of dicts)."""
+    m = _b(msg)
+    buf = (mh_span * cap)()
+    w = None if weights is None else (ctypes.c_double * ndev)(*weights)
+    k = lib.mh_multi_plan(m, len(m), lower, upper, w, ndev, buf, cap)
+    if k < 0:
+        _check(k)
+    if k > cap:
+        raise ValueError("split longer than cap")
+    return [{f: getattr(buf[i], f) for f, _ in mh_span._fields_} for i in range(k)]
+
+
+def multi_rates(devs):
+    """The per-process device rates search_multi sizes its shards by (cost units per ns, 0 = none)."""
+    arr = (ctypes.c_int * len(devs))(*devs)
+    out = (ctypes.c_double * len(devs))()
+    _check(lib.mh_multi_rates(arr, len(devs), out))
+    return list(out)
 
 
 def profile_enable(dev=0, on=True):

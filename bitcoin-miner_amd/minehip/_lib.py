@@ -25,12 +25,14 @@ MH_ENOTREQ = -6
 MH_EINTERNAL = -7
 MH_EREJECTED = -8
 OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
+MH_ABI_VERSION = 4    # include/minehip.h: the struct layouts below are this version's
 
 #: every symbol include/*.h declares
 EXPORTS = (
     "mh_abi_version", "mh_device_count", "mh_search", "mh_search_multi", "mh_hash_batch",
     "mh_last_error", "mh_msg_encode", "mh_msg_decode", "mh_miner_handle",
-    "mh_profile_enable", "mh_profile_read", "mh_profile_kernels", "mh_plan",
+    "mh_profile_enable", "mh_profile_read", "mh_profile_kernels", "mh_plan", "mh_multi_plan",
+    "mh_multi_rates",
     # minehip_server.h
     "mh_sched_default_opts", "mh_sched_create", "mh_sched_destroy", "mh_sched_add_miner",
     "mh_sched_remove_miner", "mh_sched_submit", "mh_sched_drop_client", "mh_sched_next",
@@ -51,6 +53,11 @@ class mh_kernel_stat(ctypes.Structure):
     _fields_ = [("word", ctypes.c_int32), ("mode", ctypes.c_int32), ("launches", ctypes.c_uint64),
                 ("nonces", ctypes.c_uint64), ("ns", ctypes.c_uint64), ("ops", ctypes.c_uint64),
                 ("slots", ctypes.c_uint64), ("lo_digits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class mh_span(ctypes.Structure):
+    _fields_ = [("lower", ctypes.c_uint64), ("upper", ctypes.c_uint64), ("worker", ctypes.c_int32),
+                ("kind", ctypes.c_int32), ("cost", ctypes.c_double)]
 
 
 class mh_message(ctypes.Structure):
@@ -85,6 +92,11 @@ def _load():
             f"libminehip.so not found at {LIB_PATH}; build it with `make` at the repo root "
             "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
     L = ctypes.CDLL(LIB_PATH)
+    L.mh_abi_version.restype = ctypes.c_int
+    got = L.mh_abi_version()
+    if got != MH_ABI_VERSION:
+        # a library of another ABI would read and write these structs at other strides
+        raise ImportError(f"{LIB_PATH} has ABI {got}, this binding needs {MH_ABI_VERSION}: rebuild (make)")
     u8p = ctypes.c_char_p
     sz = ctypes.c_size_t
     u64 = ctypes.c_uint64
@@ -106,6 +118,9 @@ def _load():
     L.mh_profile_kernels.argtypes = [ctypes.c_int, ctypes.POINTER(mh_kernel_stat), ctypes.c_int]
     L.mh_plan.argtypes = [u8p, sz, u64, u64, ctypes.POINTER(mh_piece), ctypes.c_int64]
     L.mh_plan.restype = ctypes.c_int64
+    L.mh_multi_plan.argtypes = [u8p, sz, u64, u64, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                ctypes.POINTER(mh_span), ctypes.c_int64]
+    L.mh_multi_rates.argtypes = [intp, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     vp = ctypes.c_void_p
     i64 = ctypes.c_int64
     L.mh_sched_default_opts.argtypes = [ctypes.POINTER(mh_sched_opts)]
@@ -125,7 +140,7 @@ def _load():
     L.mh_server_lost.argtypes = [vp, i64, u64]
     L.mh_server_pop_write.argtypes = [vp, ctypes.POINTER(i64), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     L.mh_server_stats.argtypes = [vp, ctypes.POINTER(mh_sched_stats)]
-    restype = {"mh_plan": ctypes.c_int64, "mh_last_error": ctypes.c_char_p, "mh_sched_submit": i64,
+    restype = {"mh_plan": ctypes.c_int64, "mh_multi_plan": ctypes.c_int64, "mh_last_error": ctypes.c_char_p, "mh_sched_submit": i64,
                "mh_sched_create": vp, "mh_server_create": vp, "mh_sched_default_opts": None,
                "mh_sched_destroy": None, "mh_server_destroy": None}
     for name in EXPORTS:

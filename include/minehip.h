@@ -56,7 +56,7 @@ extern "C" {
 #define MH_MAX_MSG_LEN (1u << 20)
 
 /* ABI version of this header, returned by mh_abi_version(). */
-#define MH_ABI_VERSION 3
+#define MH_ABI_VERSION 4
 
 int mh_abi_version(void);
 
@@ -72,16 +72,21 @@ int mh_device_count(void);
 int mh_search(int dev, const uint8_t *msg, size_t len, uint64_t lower, uint64_t upper,
               uint64_t *out_hash, uint64_t *out_nonce);
 
-/* Same result, the range split into chunks by the server's scheduler
- * (include/minehip_server.h) and handed to one host thread + HIP stream per
- * listed device, merged on the host by the same lexicographic min
+/* Same result, the range split over the listed devices, one host thread + HIP
+ * stream per listed device, merged on the host by the same lexicographic min
  * (associative, so bit-exact with mh_search).  No device-to-device traffic:
- * each chunk returns one 16-byte (hash, nonce).  chunk == 0: adaptive chunks
- * (250 ms of each device's measured rate -- the scheduler's default
- * target_ns, include/minehip_server.h -- capped at a fair share of what is
- * left); chunk > 0: fixed chunks of that many nonces.  A device that fails
- * hands its chunk back to the others; the call fails only if every device
- * fails (with the first failure's code). */
+ * each span returns one 16-byte (hash, nonce).
+ *   chunk == 0 (adaptive): one contiguous shard per device, sized in
+ *     proportion to the device's measured rate (kept per process across
+ *     calls; equal shards until measured), so each device runs one search.
+ *     A range of >= 2^35 nonces per device keeps its last 1/16 back as 2
+ *     chunks per device, handed out as the shards finish (mh_multi_plan
+ *     shows the split).
+ *   chunk > 0: fixed chunks of that many nonces from the server's scheduler
+ *     (include/minehip_server.h).
+ * A device that fails hands its shard or chunk back to the others; the call
+ * fails only if every device fails (with the first failure's code).  A list
+ * may repeat a device (its searches then run one after the other). */
 int mh_search_multi(const int *devs, int ndev, const uint8_t *msg, size_t len, uint64_t lower,
                     uint64_t upper, uint64_t chunk, uint64_t *out_hash, uint64_t *out_nonce);
 
@@ -186,6 +191,26 @@ typedef struct mh_piece {
  * or cap + 1 when the plan has more than cap pieces (the first cap written),
  * or a negative MH_E* code. */
 int64_t mh_plan(const uint8_t *msg, size_t len, uint64_t lower, uint64_t upper, mh_piece *out, int64_t cap);
+
+/* One span of mh_search_multi's adaptive split (chunk == 0), ABI 4. */
+typedef struct mh_span {
+    uint64_t lower, upper; /* inclusive */
+    int32_t worker;        /* head shard: index into devs; tail chunk: -1 */
+    int32_t kind;          /* 0 head shard, 1 tail chunk (handed to the first free worker) */
+    double cost;           /* relative cost (issue slots): shards ~ weights */
+} mh_span;
+
+/* Host only: how mh_search_multi(chunk = 0) would split [lower, upper] over
+ * ndev workers whose rates are in proportion to weights[0..ndev) (> 0; NULL =
+ * equal).  Head shards (worker order, empty ones omitted), then tail chunks
+ * (nonce order); together they tile [lower, upper] exactly once.  Returns the
+ * span count (cap + 1 style truncation as mh_plan) or MH_E*. */
+int64_t mh_multi_plan(const uint8_t *msg, size_t len, uint64_t lower, uint64_t upper, const double *weights,
+                      int ndev, mh_span *out, int64_t cap);
+
+/* The per-process rate table mh_search_multi sizes its shards by: out[i] =
+ * devs[i]'s measured rate in cost units per ns (0 = not measured yet). */
+int mh_multi_rates(const int *devs, int ndev, double *out);
 
 #ifdef __cplusplus
 }

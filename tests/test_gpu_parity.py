@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -263,3 +264,20 @@ print(*minehip.search(b"cmu440", {lo}, {lo + 199_999}))
     assert r.returncode == 0, r.stderr[-2000:]
     got = tuple(int(x) for x in r.stdout.split()[-2:])
     assert got == oracle.search(b"cmu440", lo, lo + 199_999, threads=4)
+
+
+@pytest.mark.gpu
+def test_code_object_without_queue_marker_runs_static(gpu):
+    """A code object loaded through the dev build's MINEHIP_DEV_CODE_OBJECT hook without the
+    work-queue marker (as one built from pre-queue sources) runs one workgroup per chunk -- every
+    chunk searched, whatever the launch's resident grid -- and gives the product's answer
+    (build/fast_search_nomarker.hsaco: the same kernels, marker removed)."""
+    from conftest import run_dev
+    co = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
+    assert os.path.exists(co), "make all builds it"
+    lo, hi = 10 ** 9, 10 ** 9 + (1 << 30) - 1  # ~1,000 chunks of fast_search<4, One> at L = 3
+    exp = gpu.search(b"cmu440", lo, hi)
+    r = run_dev(f"import minehip; print(*minehip.search(b'cmu440', {lo}, {hi}))",
+                MINEHIP_DEV_CODE_OBJECT=co, MINEHIP_MIN_LANES=1)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert tuple(int(x) for x in r.stdout.split()[-2:]) == exp

@@ -68,11 +68,24 @@ def test_search_multi_adaptive_and_fixed(gpu):
     assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0], chunk=(1 << 26) + 17) == exp
 
 
+def test_search_multi_rates_persist(gpu):
+    """Adaptive search_multi measures each device's rate on its shard (>= 2^30 nonces) and keeps
+    it for the next call's split; the answer does not depend on the split."""
+    hi = (1 << 33) - 1
+    exp = gpu.search("cmu440", 0, hi)
+    assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0]) == exp
+    r = gpu.multi_rates([0])[0]
+    assert r > 0.0
+    # slots per ns: one MI355X issues ~1e5 (nonce_cost slots ~2,000 x ~50 nonces/ns)
+    assert 1e4 < r < 1e6, r
+    assert gpu.search_multi("cmu440", 0, hi, devs=[0, 0, 0]) == exp
+
+
 def test_search_multi_device_failure_hand_back(gpu):
-    """A worker whose device fails hands its chunk back; the others finish
-    with the same answer.  If every worker fails, the call fails.  The
-    failure is injected by the dev build's MINEHIP_TEST_FAIL_WORKER hook, in a
-    child process (the product library has no hooks)."""
+    """A worker whose device fails hands its chunk (fixed chunks) or its whole shard (adaptive,
+    split over the workers still running) back; the others finish with the same answer.  If every
+    worker fails, the call fails.  The failure is injected by the dev build's
+    MINEHIP_TEST_FAIL_WORKER hook, in a child process (the product library has no hooks)."""
     from conftest import run_dev
     hi = (1 << 31) - 1
     exp = gpu.search("cmu440", 0, hi)
@@ -80,12 +93,15 @@ def test_search_multi_device_failure_hand_back(gpu):
 import os, minehip
 os.environ["MINEHIP_TEST_FAIL_WORKER"] = "1"
 print(*minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0, 0], chunk=1 << 27))
+print(*minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0, 0]))
 os.environ["MINEHIP_TEST_FAIL_WORKER"] = "0"   # the only worker fails
-try:
-    minehip.search_multi("cmu440", 0, {hi}, devs=[0], chunk=1 << 27)
-    raise SystemExit("search_multi succeeded with its only worker failing")
-except minehip.MinehipError as e:
-    assert e.code == minehip.MH_EHIP and "injected" in str(e), e
+for chunk in (1 << 27, 0):
+    try:
+        minehip.search_multi("cmu440", 0, {hi}, devs=[0], chunk=chunk)
+        raise SystemExit("search_multi succeeded with its only worker failing")
+    except minehip.MinehipError as e:
+        assert e.code == minehip.MH_EHIP and "injected" in str(e), e
 """)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert tuple(int(x) for x in r.stdout.split()[-2:]) == exp
+    lines = r.stdout.strip().splitlines()[-2:]
+    assert [tuple(int(x) for x in ln.split()) for ln in lines] == [exp, exp]

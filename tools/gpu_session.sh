@@ -25,6 +25,8 @@ for s in $STEPS; do
     info)
       (rocminfo 2>&1 | grep -E 'Marketing Name|Name: +gfx|Compute Unit|Max Clock|SIMDs per CU' | head -20
        nproc; grep -m1 'model name' /proc/cpuinfo; echo "OMP_NUM_THREADS=${OMP_NUM_THREADS:-}"
+       python3 -c "import os; print('affinity cores', len(os.sched_getaffinity(0)))"
+       echo "cgroup cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null || echo none)"
        (go version || echo "no go") 2>&1
        amd-smi static --clock 2>/dev/null | head -40) > "$OUT/info.txt" 2>&1
       ;;
@@ -77,6 +79,16 @@ for s in $STEPS; do
           -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --no-clock > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
+      # the per-(kernel, queue) summary that recomputes roofline.frac (tools/trace_frac.py)
+      tr=$(find "$OUT/prof" -name '*kernel_trace.csv' | head -1)
+      python3 "$ROOT/tools/trace_frac.py" "$OUT/prof_bench.json" "$tr" --stats-out "$OUT/kernel_stats_by_queue.csv" \
+          > "$OUT/trace_frac.json" 2>&1; cat "$OUT/trace_frac.json"
+      ;;
+    inproc)
+      # the in-process N-GPU path (mh_search_multi) modelled on this GPU: round-3 scheduler chain
+      # against round-4 shards, configs[3] steps at N = 2, 4, 8 (tools/inproc_model.py)
+      timeout -k 10 600 python "$ROOT/tools/inproc_model.py" --out "$OUT/inproc_model.json" > "$OUT/inproc.log" 2>&1
+      rc=$?; echo "inproc rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/inproc.log"; fatal $rc
       ;;
     pmc)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
