@@ -1,0 +1,105 @@
+"""One A/B driver for every kernel / plan experiment: a recipe names the variants (environment
+settings of the planner knobs, or MINEHIP_DEV_CODE_OBJECT code objects for the dev build) and
+the workloads; each workload is one tools/kbench.py process that interleaves the variants round
+by round, so an A/B shares one box and one clock.  Run on the GPU box:
+
+  python tools/ab.py tools/ab/<recipe>.json [--tag r04x] [--only d10,cfg1] [--dry-run]
+
+writes gpurun_out/<tag>/kbench_<workload>.json (+ .err) and stops at the first failing step
+(a GPU fault, abort or time limit ends the session: nothing more runs on the GPU).
+
+Recipe (JSON):
+  {"about": "...", "tag": "r03u",
+   "variants": {"name": "K=V,K=V" | "", ...},          # "" = the product build as is
+   "code_objects": {"name": "build/ab/x.hsaco"},       # shorthand: MINEHIP_DEV_CODE_OBJECT=...
+   "workloads": [["d10", 7, "clock"], ["cfg1", 9], ...]}  # WORKLOADS name, rounds, optional clock
+The recipes under tools/ab/ are the experiments behind DESIGN.md and profiles/ (HISTORY.md).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# name -> (message, first nonce, nonces): BASELINE workloads and the buckets the A/Bs isolate
+WORKLOADS = {
+    "d10": ("cmu440", 10 ** 9, 1 << 32),                  # configs[1]'s d = 10 bucket layout, <4, One>
+    "d9": ("cmu440", 10 ** 8, 9 * 10 ** 8),               # d = 9, <3, One>
+    "d79": ("cmu440", 10 ** 6, 999 * 10 ** 6),            # d = 7..9
+    "cfg1": ("cmu440", 0, 1 << 32),                       # BASELINE configs[1], whole
+    "cfg3a": ("a" * 100, 0, 1 << 34),                     # configs[2]: host midstate block
+    "cfg3b": ("x" * 60, 0, 1 << 34),                      # configs[2]: two tail blocks
+    "cfg4slice": ("cmu440", 1 << 39, 1 << 36),            # a 2^36 slice of configs[3]
+    "cfg4step": ("cmu440", 1 << 39, (1 << 40) // 20),     # one of configs[3]'s 20 bench steps
+    "shard8": ("cmu440", 1 << 39, 6871947673),            # one 8-GPU shard of a configs[3] step
+    "p55": (("cmu440-" * 10)[:55], 0, 1 << 32),           # <13|14|15, Two> layouts
+}
+FATAL = {124, 134, 137, 139}
+
+
+def load(path):
+    with open(path) as f:
+        r = json.load(f)
+    variants = dict(r.get("variants", {}))
+    for name, co in r.get("code_objects", {}).items():
+        variants[name] = f"MINEHIP_DEV_CODE_OBJECT={co}"
+    if not variants or not r.get("workloads"):
+        raise SystemExit(f"{path}: a recipe needs variants and workloads")
+    for w in r["workloads"]:
+        if w[0] not in WORKLOADS:
+            raise SystemExit(f"{path}: unknown workload {w[0]!r} (known: {', '.join(WORKLOADS)})")
+    return r, variants
+
+
+def commands(recipe, variants, only=None):
+    """[(workload name, argv)] of the kbench processes a recipe runs."""
+    out = []
+    for w in recipe["workloads"]:
+        name, rounds = w[0], int(w[1])
+        if only and name not in only:
+            continue
+        msg, lo, count = WORKLOADS[name]
+        argv = [sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--msg", msg, "--lo", str(lo),
+                "--count", str(count), "--rounds", str(rounds)]
+        if "clock" in w[2:]:
+            argv.append("--clock")
+        for v, env in variants.items():
+            argv += ["--var", f"{v}:{env}"]
+        out.append((name, argv))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("recipe")
+    ap.add_argument("--tag", default=None, help="output directory under gpurun_out/ (default: the recipe's)")
+    ap.add_argument("--only", default=None, help="comma-separated workloads to run")
+    ap.add_argument("--timeout", type=int, default=400, help="seconds per kbench process")
+    ap.add_argument("--dry-run", action="store_true")
+    a = ap.parse_args()
+    recipe, variants = load(a.recipe)
+    out = os.path.join(ROOT, "gpurun_out", a.tag or recipe.get("tag", "ab"))
+    cmds = commands(recipe, variants, set(a.only.split(",")) if a.only else None)
+    if a.dry_run:
+        for name, argv in cmds:
+            print(name, " ".join(argv[1:]))
+        return
+    os.makedirs(out, exist_ok=True)
+    for name, argv in cmds:
+        with open(os.path.join(out, f"kbench_{name}.json"), "w") as fo, \
+                open(os.path.join(out, f"kbench_{name}.err"), "w") as fe:
+            try:
+                rc = subprocess.run(["timeout", "-k", "10", str(a.timeout), *argv], stdout=fo, stderr=fe).returncode
+            except KeyboardInterrupt:
+                raise SystemExit(130)
+        print(f"{name}: rc={rc}", flush=True)
+        with open(os.path.join(out, f"kbench_{name}.json")) as f:
+            print(f.read().strip(), flush=True)
+        if rc != 0:
+            raise SystemExit(rc if rc in FATAL or rc > 128 else 1)
+
+
+if __name__ == "__main__":
+    main()
