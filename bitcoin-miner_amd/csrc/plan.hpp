@@ -115,7 +115,7 @@ struct CostSeg {
     uint64_t a, b;  // inclusive
     double per;
 };
-constexpr double kGenericSlotsPerBlock = 4.0 * 1760.0;  // formatting + a full compression, scalar-ish
+constexpr double kGenericSlotsPerBlock = 2.0 * 1760.0;  // estimate: a full compression + per-nonce formatting
 void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
                    std::vector<CostSeg>* out);
 double segments_cost(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi);
