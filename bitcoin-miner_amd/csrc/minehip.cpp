@@ -12,6 +12,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -773,7 +774,7 @@ int64_t mh_multi_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t u
     std::vector<double> w((size_t)ndev, 1.0);
     if (weights)
         for (int i = 0; i < ndev; ++i) {
-            if (!(weights[i] > 0.0)) return fail(MH_EINVAL, "weights must be > 0");
+            if (!(weights[i] > 0.0) || !std::isfinite(weights[i])) return fail(MH_EINVAL, "weights must be finite and > 0");
             w[(size_t)i] = weights[i];
         }
     mh::Prefix pre;

@@ -85,6 +85,9 @@ def test_split_argument_errors():
     with pytest.raises(minehip.MinehipError) as e:
         minehip.multi_plan(b"x", 0, 4, 2, [1.0, 0.0])
     assert e.value.code == minehip.MH_EINVAL
+    for bad in (float("inf"), float("nan"), -1.0):
+        with pytest.raises(minehip.MinehipError):
+            minehip.multi_plan(b"x", 0, 4, 2, [1.0, bad])
     with pytest.raises(minehip.MinehipError) as e:
         minehip.multi_plan(b"x", 0, 4, 0)
     assert e.value.code == minehip.MH_EINVAL
