@@ -917,8 +917,8 @@ def main():
                        "kernel_clock_ghz": p.get("kernel_clock_ghz")}
                       for p in per_dev]
         if multi:  # the rates the library sized the last step's shards by (cost units per ns)
-            for pd, r in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
-                pd["multi_rate"] = round(r, 1)
+            for pd, rate in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
+                pd["multi_rate"] = round(rate, 1)
         line = {
             "metric": METRIC,
             "value": round(value, 4),

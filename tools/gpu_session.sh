@@ -76,7 +76,7 @@ for s in $STEPS; do
       ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-          -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --no-clock > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+          -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --no-clock --no-n1 > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
       rc=$?; echo "prof rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       find "$OUT/prof" -name '*kernel_stats.csv' -exec cat {} \; | head -20
       # the per-(kernel, queue) summary that recomputes roofline.frac (tools/trace_frac.py)
@@ -179,6 +179,13 @@ for s in $STEPS; do
           --master-addr 127.0.0.1 --master-port 29535 "$ROOT/bench.py" --gpus 8 --config 2 --bits 28 --steps 2 \
           --warmup 1 > "$OUT/dist8_weak.json" 2> "$OUT/dist8_weak.err"
       rc=$?; echo "dist8 weak rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8_weak.json"; fatal $rc
+      ;;
+    ab:*)
+      # an A/B recipe (tools/ab.py, tools/ab/<recipe>.json): one kbench process per workload
+      recipe=${s#ab:}
+      timeout -k 10 1500 python "$ROOT/tools/ab.py" "$ROOT/tools/ab/$recipe.json" --tag "$TAG/ab_$recipe" \
+          > "$OUT/ab_$recipe.log" 2>&1
+      rc=$?; echo "ab $recipe rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/ab_$recipe.log"; fatal $rc
       ;;
     *) echo "unknown step $s";;
   esac
