@@ -225,7 +225,7 @@ bool bucket_layout(const Prefix& pre, int d, uint64_t A, uint64_t B, const PlanO
     L = std::min(L, 5);
     // A lane runs 10^L nonces serially: a bucket with few runs would leave
     // most SIMDs idle and end in a long tail, so shorten the runs until
-    // the bucket has min_lanes of them (2^21: ~8 workgroups per CU).
+    // the bucket has min_lanes of them (2^19: ~8 workgroups per CU, one generation of the grid).
     while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
     while (L >= 1 && !make_fast_args(pre, d, L, J, mode, nb, fa)) --L;
     *L_out = L;

@@ -56,7 +56,12 @@ struct PlanOpts {
     // +3% on configs[3] against L <= 2, 2^23 runs, 2^32-nonce launches, the
     // round-1 choice (profiles/r02ap_kbench_plan.json).
     int lower_digits = 3;                        // L upper bound (nonces per lane = 10^L)
-    uint64_t min_lanes = 1u << 21;               // lower L until a bucket has this many runs
+    // Lower L until a bucket has min_lanes runs: 2^19 runs = 2,048 workgroups, about one generation
+    // of the resident grid (7 x 256 CUs).  Round 4, with work queues and two streams, A/B in one
+    // process against the round-2 2^21: configs[1] +1.4% (its d = 9 bucket now runs 1,000-nonce
+    // lanes), configs[2] +0.4% / +0.6%; 2^16 (buckets of a fifth of a generation at L = 3) -4.7%
+    // (profiles/r04c_kbench_min_lanes_*.json).
+    uint64_t min_lanes = 1u << 19;
     uint64_t max_nonces_per_launch = 1ull << 34; // one launch <= ~0.35 s (one tail block) / ~0.6 s (two)
     uint32_t max_blocks = 1u << 17;              // workgroups per launch (<= kMaxBlocksPerLaunch; +0.1% over 2^16)
     uint64_t generic_below = 1u << 20;           // a bucket this small goes to the generic kernel whole
