@@ -199,7 +199,9 @@ int flush_partials(DevCtx* c, bool split) {
 // Enqueue one piece on the context's stream.  Its workgroups write their
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
-bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) { return p.kind == 0 && p.L == opt.lower_digits; }
+bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) {
+    return p.kind == 0 && p.L == opt.lower_digits && p.count >= opt.coarse_min;
+}
 
 int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
     // split: coarse pieces (the full L) on the high-priority stream, the rest on the low one
@@ -279,6 +281,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //                          2^28; 0: none)
 //   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
 //                          XCDs take more; default); 0: one workgroup per chunk
+//   MINEHIP_COARSE_MIN     full-L pieces smaller than this go to the low-priority stream (0)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -304,6 +307,7 @@ mh::PlanOpts plan_opts() {
         const int v = atoi(e);
         if (v == 0 || v == 1) o.queue = v;
     }
+    if (const char* e = getenv("MINEHIP_COARSE_MIN")) o.coarse_min = strtoull(e, nullptr, 10);
     return o;
 }
 

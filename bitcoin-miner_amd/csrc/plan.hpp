@@ -83,6 +83,9 @@ struct PlanOpts {
     // with the same code object: +0.6% to +1.9% on configs[1], configs[2]'s halves and the d = 10
     // bucket (profiles/r03u_*).  0: one workgroup per chunk.
     int queue = 1;
+    // Execution: a full-L piece goes to the high-priority stream only if it has at least coarse_min
+    // nonces (smaller ones back-fill from the low-priority stream).  0: every full-L piece.
+    uint64_t coarse_min = 0;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb
