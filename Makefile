@@ -5,10 +5,10 @@ PKG     := bitcoin-miner_amd
 CSRC    := $(PKG)/csrc
 LIB     := $(PKG)/minehip/libminehip.so
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
-SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSRC)/message.cpp \
+SRCS    := $(CSRC)/search_kernels.hip $(CSRC)/minehip.cpp $(CSRC)/plan.cpp $(CSRC)/multi.cpp $(CSRC)/message.cpp \
            $(CSRC)/sched.cpp $(CSRC)/server.cpp
 HDRS    := $(CSRC)/layout.hpp $(CSRC)/plan.hpp $(CSRC)/sha256_gfx950.hpp $(CSRC)/msgcodec.hpp \
-           $(CSRC)/sched.hpp $(CSRC)/kernel_common.hpp include/minehip.h include/minehip_server.h
+           $(CSRC)/sched.hpp $(CSRC)/multi.hpp $(CSRC)/kernel_common.hpp include/minehip.h include/minehip_server.h
 LLVM    ?= /opt/rocm/lib/llvm/bin
 BUILD   := build
 FAST_HDRS := $(CSRC)/kernel_common.hpp $(CSRC)/layout.hpp $(CSRC)/sha256_gfx950.hpp

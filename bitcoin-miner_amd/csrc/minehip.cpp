@@ -14,7 +14,6 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
-#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -24,6 +23,7 @@
 #include "../../include/minehip.h"
 #include "../../include/minehip_server.h"
 #include "layout.hpp"
+#include "multi.hpp"
 #include "plan.hpp"
 #include "sched.hpp"
 
@@ -380,150 +380,6 @@ int check_common(const uint8_t* msg, size_t len) {
     return MH_OK;
 }
 
-// ---- mh_search_multi with adaptive shards (chunk == 0) ------------------------------------
-// Each worker (one listed device) gets ONE contiguous head shard up front, sized in proportion to
-// its device's measured rate, so a step of the multi-GPU search is one search per device: one plan,
-// full-size launches, one drain, one sync.  A range large enough that a few percent of it still
-// makes long chunks (>= 2^35 nonces per worker, ~0.6 s) keeps its last 1/16 back as 2 chunks per
-// worker, handed out as the heads finish, which absorbs a device running slower than its rate
-// predicted.  Rates persist across calls (the per-process table below), in cost units per ns
-// (plan.hpp CostSeg: issue slots), so a shard holding short-lane buckets or the generic kernel's
-// edges does not make its device look slow.  Before any rate is known the shards are equal.
-constexpr uint64_t kTailMinPerWorker = 1ull << 35;
-constexpr int kTailDiv = 16;
-constexpr uint64_t kRateMinNonces = 1ull << 30;  // shorter searches are latency, not rate
-
-std::mutex g_rate_mu;
-std::vector<double> g_rate;  // per device: slots per ns (EWMA over its searches), 0 = not measured
-
-std::vector<double> worker_weights(const int* devs, int ndev) {
-    std::lock_guard<std::mutex> lk(g_rate_mu);
-    std::vector<double> w((size_t)ndev, 0.0);
-    double sum = 0.0;
-    int known = 0;
-    for (int i = 0; i < ndev; ++i) {
-        const double r = (size_t)devs[i] < g_rate.size() ? g_rate[(size_t)devs[i]] : 0.0;
-        w[(size_t)i] = r;
-        if (r > 0.0) {
-            sum += r;
-            ++known;
-        }
-    }
-    const double fill = known ? sum / known : 1.0;
-    for (auto& x : w)
-        if (x <= 0.0) x = fill;
-    return w;
-}
-
-void record_rate(int dev, double slots, uint64_t ns) {
-    if (ns == 0 || slots <= 0.0) return;
-    std::lock_guard<std::mutex> lk(g_rate_mu);
-    if ((size_t)dev >= g_rate.size()) g_rate.resize((size_t)dev + 1, 0.0);
-    const double r = slots / (double)ns;
-    g_rate[(size_t)dev] = g_rate[(size_t)dev] > 0.0 ? 0.5 * g_rate[(size_t)dev] + 0.5 * r : r;
-}
-
-struct MultiPlan {
-    std::vector<mh::CostSeg> segs;
-    std::vector<mh::Span> head;  // one per worker (may be empty)
-    std::vector<mh::Span> tail;  // non-empty, in nonce order
-};
-
-void multi_plan(const mh::Prefix& pre, uint64_t lower, uint64_t upper, const std::vector<double>& w,
-                MultiPlan* mp) {
-    mh::cost_segments(pre, lower, upper, plan_opts(), &mp->segs);
-    const size_t n = w.size();
-    const unsigned __int128 total = (unsigned __int128)(upper - lower) + 1u;
-    const size_t T = (n > 1 && total / n >= kTailMinPerWorker) ? 2 * n : 0;
-    std::vector<double> ww = w;
-    double wsum = 0.0;
-    for (double x : w) wsum += x;
-    for (size_t k = 0; k < T; ++k) ww.push_back(wsum / (double)(kTailDiv - 1) / (double)T);  // tail = 1/16
-    std::vector<mh::Span> all;
-    mh::split_by_cost(mp->segs, ww, &all);
-    mp->head.assign(all.begin(), all.begin() + (ptrdiff_t)n);
-    mp->tail.clear();
-    for (size_t k = n; k < all.size(); ++k)
-        if (!all[k].empty) mp->tail.push_back(all[k]);
-}
-
-// The span split into `parts` contiguous near-equal pieces (a failed worker's span, handed back).
-std::vector<mh::Span> split_even(const mh::Span& s, int parts) {
-    std::vector<mh::Span> out;
-    const unsigned __int128 n = (unsigned __int128)(s.hi - s.lo) + 1u;
-    unsigned __int128 prev = 0;
-    for (int k = 1; k <= parts; ++k) {
-        const unsigned __int128 pos = n * (unsigned)k / (unsigned)parts;
-        if (pos > prev) out.push_back(mh::Span{(uint64_t)(s.lo + prev), (uint64_t)(s.lo + (pos - 1u)), false});
-        prev = pos;
-    }
-    return out;
-}
-
-int search_multi_shards(const int* devs, int ndev, const mh::Prefix& pre, uint64_t lower, uint64_t upper,
-                        int fail_worker, uint64_t* out_hash, uint64_t* out_nonce) {
-    MultiPlan mp;
-    multi_plan(pre, lower, upper, worker_weights(devs, ndev), &mp);
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<mh::Span> queue(mp.tail.begin(), mp.tail.end());
-    int outstanding = 0, alive = ndev, first_err = 0;
-    for (const auto& s : mp.head) outstanding += s.empty ? 0 : 1;
-    std::string err_msg;
-    uint64_t bh = ~0ull, bn = ~0ull;
-    bool any = false;
-    std::vector<std::thread> th;
-    for (int i = 0; i < ndev; ++i) {
-        th.emplace_back([&, i]() {
-            mh::Span cur = mp.head[(size_t)i];
-            bool have = !cur.empty;
-            for (;;) {
-                if (have) {
-                    uint64_t h = 0, nn = 0, ns = 0;
-                    const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
-                                                     : search_impl(devs[i], pre, cur.lo, cur.hi, &h, &nn, &ns);
-                    if (r == MH_OK && cur.hi - cur.lo >= kRateMinNonces - 1u)
-                        record_rate(devs[i], mh::segments_cost(mp.segs, cur.lo, cur.hi), ns);
-                    std::lock_guard<std::mutex> lk(mu);
-                    --outstanding;
-                    if (r != MH_OK) {
-                        // hand the span back, cut for the workers still running, and leave
-                        if (!first_err) {
-                            first_err = r;
-                            err_msg = g_err;
-                        }
-                        --alive;
-                        const auto parts = split_even(cur, std::max(1, alive));
-                        queue.insert(queue.begin(), parts.begin(), parts.end());
-                        cv.notify_all();
-                        return;
-                    }
-                    if (!any || h < bh || (h == bh && nn < bn)) {
-                        bh = h;
-                        bn = nn;
-                        any = true;
-                    }
-                    cv.notify_all();
-                }
-                std::unique_lock<std::mutex> lk(mu);
-                // wait for work: a tail chunk, or a span a failed worker handed back
-                cv.wait(lk, [&] { return !queue.empty() || outstanding == 0; });
-                if (queue.empty()) return;  // nothing queued and nothing running: done
-                cur = queue.front();
-                queue.pop_front();
-                ++outstanding;
-                have = true;
-            }
-        });
-    }
-    for (auto& t : th) t.join();
-    if (!queue.empty() || !any)
-        return fail(first_err ? first_err : MH_EHIP, err_msg.empty() ? "every device failed" : err_msg);
-    *out_hash = bh;
-    *out_nonce = bn;
-    return MH_OK;
-}
-
 }  // namespace
 
 extern "C" {
@@ -569,8 +425,19 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
 #endif
     if (ndev == 1 && chunk == 0 && fail_worker < 0)
         return search_impl(devs[0], pre, lower, upper, out_hash, out_nonce);
-    // Adaptive: one rate-weighted shard per device (+ a short dynamic tail on long ranges).
-    if (chunk == 0) return search_multi_shards(devs, ndev, pre, lower, upper, fail_worker, out_hash, out_nonce);
+    // Adaptive: one rate-weighted shard per device (+ a short dynamic tail on long ranges), multi.hpp.
+    if (chunk == 0) {
+        const mh::SpanSearch search = [&](int worker, int dev, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* n,
+                                          uint64_t* ns, std::string* err) {
+            const int r = (worker == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
+                                                  : search_impl(dev, pre, lo, hi, h, n, ns);
+            if (r) *err = g_err;  // this worker thread's description
+            return r;
+        };
+        std::string err;
+        const int r = mh::search_shards(devs, ndev, pre, lower, upper, plan_opts(), search, out_hash, out_nonce, &err);
+        return r ? fail(r, err) : MH_OK;
+    }
     // Fixed chunks: one miner per listed device, fed by the server's scheduler (sched.hpp) with
     // chunks of exactly `chunk` nonces.  A device that fails hands its chunk back to the others.
     mh_sched_opts o;
@@ -783,8 +650,8 @@ int64_t mh_multi_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t u
         }
     mh::Prefix pre;
     mh::absorb_prefix(msg, len, &pre);
-    MultiPlan mp;
-    multi_plan(pre, lower, upper, w, &mp);
+    mh::MultiPlan mp;
+    mh::multi_plan(pre, lower, upper, plan_opts(), w, &mp);
     int64_t k = 0;
     auto put = [&](const mh::Span& s, int worker, int kind) {
         if (k < cap && out) {
@@ -805,9 +672,7 @@ int64_t mh_multi_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t u
 int mh_multi_rates(const int* devs, int ndev, double* out) {
     g_err.clear();
     if (!devs || !out || ndev < 0) return fail(MH_EINVAL, "bad arguments");
-    std::lock_guard<std::mutex> lk(g_rate_mu);
-    for (int i = 0; i < ndev; ++i)
-        out[i] = (devs[i] >= 0 && (size_t)devs[i] < g_rate.size()) ? g_rate[(size_t)devs[i]] : 0.0;
+    for (int i = 0; i < ndev; ++i) out[i] = mh::device_rate(devs[i]);
     return MH_OK;
 }
 

@@ -1,0 +1,149 @@
+// multi.cpp -- see multi.hpp.
+#include "multi.hpp"
+
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+
+#include "../../include/minehip.h"
+
+namespace mh {
+namespace {
+
+std::mutex g_rate_mu;
+std::vector<double> g_rate;  // per device: slots per ns (EWMA over its searches), 0 = not measured
+
+// The span split into `parts` contiguous near-equal pieces (a failed worker's span, handed back).
+std::vector<Span> split_even(const Span& s, int parts) {
+    std::vector<Span> out;
+    const unsigned __int128 n = (unsigned __int128)(s.hi - s.lo) + 1u;
+    unsigned __int128 prev = 0;
+    for (int k = 1; k <= parts; ++k) {
+        const unsigned __int128 pos = n * (unsigned)k / (unsigned)parts;
+        if (pos > prev) out.push_back(Span{(uint64_t)(s.lo + prev), (uint64_t)(s.lo + (pos - 1u)), false});
+        prev = pos;
+    }
+    return out;
+}
+
+}  // namespace
+
+std::vector<double> worker_weights(const int* devs, int ndev) {
+    std::lock_guard<std::mutex> lk(g_rate_mu);
+    std::vector<double> w((size_t)ndev, 0.0);
+    double sum = 0.0;
+    int known = 0;
+    for (int i = 0; i < ndev; ++i) {
+        const double r = (devs[i] >= 0 && (size_t)devs[i] < g_rate.size()) ? g_rate[(size_t)devs[i]] : 0.0;
+        w[(size_t)i] = r;
+        if (r > 0.0) {
+            sum += r;
+            ++known;
+        }
+    }
+    const double fill = known ? sum / known : 1.0;
+    for (auto& x : w)
+        if (x <= 0.0) x = fill;
+    return w;
+}
+
+void record_rate(int dev, double slots, uint64_t ns) {
+    if (dev < 0 || ns == 0 || slots <= 0.0) return;
+    std::lock_guard<std::mutex> lk(g_rate_mu);
+    if ((size_t)dev >= g_rate.size()) g_rate.resize((size_t)dev + 1, 0.0);
+    const double r = slots / (double)ns;
+    g_rate[(size_t)dev] = g_rate[(size_t)dev] > 0.0 ? 0.5 * g_rate[(size_t)dev] + 0.5 * r : r;
+}
+
+double device_rate(int dev) {
+    std::lock_guard<std::mutex> lk(g_rate_mu);
+    return (dev >= 0 && (size_t)dev < g_rate.size()) ? g_rate[(size_t)dev] : 0.0;
+}
+
+void multi_plan(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
+                const std::vector<double>& w, MultiPlan* mp) {
+    cost_segments(pre, lower, upper, opt, &mp->segs);
+    const size_t n = w.size();
+    const unsigned __int128 total = (unsigned __int128)(upper - lower) + 1u;
+    const size_t T = (n > 1 && total / n >= kTailMinPerWorker) ? 2 * n : 0;
+    std::vector<double> ww = w;
+    double wsum = 0.0;
+    for (double x : w) wsum += x;
+    for (size_t k = 0; k < T; ++k) ww.push_back(wsum / (double)(kTailDiv - 1) / (double)T);  // tail = 1/16
+    std::vector<Span> all;
+    split_by_cost(mp->segs, ww, &all);
+    mp->head.assign(all.begin(), all.begin() + (ptrdiff_t)n);
+    mp->tail.clear();
+    for (size_t k = n; k < all.size(); ++k)
+        if (!all[k].empty) mp->tail.push_back(all[k]);
+}
+
+int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, uint64_t upper,
+                  const PlanOpts& opt, const SpanSearch& search, uint64_t* out_hash, uint64_t* out_nonce,
+                  std::string* err) {
+    MultiPlan mp;
+    multi_plan(pre, lower, upper, opt, worker_weights(devs, ndev), &mp);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Span> queue(mp.tail.begin(), mp.tail.end());
+    int outstanding = 0, alive = ndev, first_err = 0;
+    for (const auto& s : mp.head) outstanding += s.empty ? 0 : 1;
+    std::string err_msg;
+    uint64_t bh = ~0ull, bn = ~0ull;
+    bool any = false;
+    auto worker = [&](int i) {
+        Span cur = mp.head[(size_t)i];
+        bool have = !cur.empty;
+        for (;;) {
+            if (have) {
+                uint64_t h = 0, nn = 0, ns = 0;
+                std::string e;
+                const int r = search(i, devs[i], cur.lo, cur.hi, &h, &nn, &ns, &e);
+                if (r == MH_OK && cur.hi - cur.lo >= kRateMinNonces - 1u)
+                    record_rate(devs[i], segments_cost(mp.segs, cur.lo, cur.hi), ns);
+                std::lock_guard<std::mutex> lk(mu);
+                --outstanding;
+                if (r != MH_OK) {
+                    // hand the span back, cut for the workers still running, and leave
+                    if (!first_err) {
+                        first_err = r;
+                        err_msg = e;
+                    }
+                    --alive;
+                    const auto parts = split_even(cur, std::max(1, alive));
+                    queue.insert(queue.begin(), parts.begin(), parts.end());
+                    cv.notify_all();
+                    return;
+                }
+                if (!any || h < bh || (h == bh && nn < bn)) {
+                    bh = h;
+                    bn = nn;
+                    any = true;
+                }
+                cv.notify_all();
+            }
+            std::unique_lock<std::mutex> lk(mu);
+            // wait for work: a tail chunk, or a span a failed worker handed back
+            cv.wait(lk, [&] { return !queue.empty() || outstanding == 0; });
+            if (queue.empty()) return;  // nothing queued and nothing running: done
+            cur = queue.front();
+            queue.pop_front();
+            ++outstanding;
+            have = true;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 0; i < ndev; ++i) th.emplace_back(worker, i);
+    for (auto& t : th) t.join();
+    if (!queue.empty() || !any) {
+        *err = err_msg.empty() ? "every device failed" : err_msg;
+        return first_err ? first_err : MH_EHIP;
+    }
+    *out_hash = bh;
+    *out_nonce = bn;
+    return MH_OK;
+}
+
+}  // namespace mh

@@ -1,0 +1,128 @@
+// tsan_multi.cpp -- mh_search_multi's shard coordinator (bitcoin-miner_amd/csrc/multi.cpp) driven
+// with a stand-in search from up to 8 worker threads, built with -fsanitize=thread by
+// tests/test_host_sanitize.py.  The GPU search is replaced by a recorder: each span it is handed
+// "finds" a deterministic (hash, nonce) of the span, sleeps a little, and some workers fail
+// (any of them, possibly all).  Invariants, for random ranges (up to 2^64 - 1, long enough for the
+// dynamic tail) and random device lists (repeats allowed):
+//   * success <=> at least one worker survived;
+//   * the successful spans tile [lower, upper] exactly once (a failed worker's span is handed back
+//     and searched by the others);
+//   * the result is the lexicographic minimum over the successful spans;
+//   * a failure returns the failing search's code and text;
+//   * rates are recorded for the devices whose searches of >= 2^30 nonces succeeded.
+//
+//   tsan_multi <seed> <iterations>     exit 0 = every invariant held
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <random>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../bitcoin-miner_amd/csrc/multi.hpp"
+#include "../../include/minehip.h"
+
+static int g_fail = 0;
+#define CHECK(c)                                                                  \
+    do {                                                                          \
+        if (!(c)) {                                                               \
+            fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+            ++g_fail;                                                             \
+            return;                                                               \
+        }                                                                         \
+    } while (0)
+
+static uint64_t splitmix(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+struct Rec {
+    uint64_t lo, hi, h, n;
+};
+
+static void one_case(std::mt19937_64& rng, int it) {
+    const int ndev = 1 + (int)(rng() % 8);
+    std::vector<int> devs((size_t)ndev);
+    for (auto& d : devs) d = (int)(rng() % 4);
+    std::vector<bool> fails((size_t)ndev, false);
+    const int mode = (int)(rng() % 4);  // 0: none fail, 1: one, 2: random set, 3: all
+    for (int i = 0; i < ndev; ++i)
+        fails[(size_t)i] = mode == 3 || (mode == 1 && i == (int)(rng() % ndev)) || (mode == 2 && rng() % 3 == 0);
+    uint64_t lower, upper;
+    switch (rng() % 4) {
+        case 0: lower = rng() % 100000; upper = lower + rng() % 50000; break;
+        case 1: lower = rng() % (1ull << 40); upper = lower + (rng() % 3 + 1) * ((uint64_t)ndev << 35); break;
+        case 2: lower = ~0ull - (rng() % (1ull << 44)); upper = ~0ull; break;
+        default: lower = 0; upper = ~0ull; break;
+    }
+    const std::string msg = (it % 2) ? "cmu440" : std::string(60, 'x');
+    mh::Prefix pre;
+    mh::absorb_prefix((const uint8_t*)msg.data(), msg.size(), &pre);
+    std::mutex mu;
+    std::vector<Rec> done;
+    std::atomic<int> calls{0};
+    const mh::SpanSearch search = [&](int worker, int dev, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* n,
+                                      uint64_t* ns, std::string* err) -> int {
+        (void)dev;
+        calls++;
+        std::this_thread::sleep_for(std::chrono::microseconds(splitmix(lo ^ (uint64_t)worker) % 300));
+        if (fails[(size_t)worker]) {
+            *err = "stand-in failure of worker " + std::to_string(worker);
+            return MH_EHIP;
+        }
+        *h = splitmix(lo * 31 + hi);
+        *n = lo + splitmix(hi) % (hi - lo + 1 == 0 ? 1 : hi - lo + 1);
+        *ns = 1 + (hi - lo) / 50;  // ~50 nonces per ns
+        std::lock_guard<std::mutex> lk(mu);
+        done.push_back(Rec{lo, hi, *h, *n});
+        return MH_OK;
+    };
+    mh::PlanOpts opt;
+    uint64_t oh = 0, on = 0;
+    std::string err;
+    const int rc = mh::search_shards(devs.data(), ndev, pre, lower, upper, opt, search, &oh, &on, &err);
+    const bool survivor = std::count(fails.begin(), fails.end(), false) > 0;
+    if (!survivor) {
+        CHECK(rc == MH_EHIP);
+        CHECK(err.find("stand-in failure") == 0);
+        return;
+    }
+    CHECK(rc == MH_OK);
+    std::sort(done.begin(), done.end(), [](const Rec& a, const Rec& b) { return a.lo < b.lo; });
+    CHECK(!done.empty() && done.front().lo == lower && done.back().hi == upper);
+    for (size_t k = 1; k < done.size(); ++k) CHECK(done[k - 1].hi + 1 == done[k].lo);
+    uint64_t bh = ~0ull, bn = ~0ull;
+    for (const auto& r : done)
+        if (r.h < bh || (r.h == bh && r.n < bn)) {
+            bh = r.h;
+            bn = r.n;
+        }
+    CHECK(oh == bh && on == bn);
+    for (const auto& r : done)
+        if (r.hi - r.lo >= mh::kRateMinNonces - 1u) {
+            // some device searched this span and recorded a rate (which one is not recorded here)
+            bool any = false;
+            for (int d : devs) any = any || mh::device_rate(d) > 0.0;
+            CHECK(any);
+            break;
+        }
+}
+
+int main(int argc, char** argv) {
+    const uint64_t seed = argc > 1 ? strtoull(argv[1], nullptr, 10) : 440;
+    const int iters = argc > 2 ? atoi(argv[2]) : 100;
+    std::mt19937_64 rng(seed);
+    for (int it = 0; it < iters; ++it) one_case(rng, it);
+    printf("iterations=%d failures=%d\n", iters, g_fail);
+    return g_fail ? 1 : 0;
+}
