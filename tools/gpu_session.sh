@@ -180,6 +180,18 @@ for s in $STEPS; do
           --warmup 1 > "$OUT/dist8_weak.json" 2> "$OUT/dist8_weak.err"
       rc=$?; echo "dist8 weak rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8_weak.json"; fatal $rc
       ;;
+    rehearse8)
+      # the N = 8 configs[3] lines end to end on the box's one GPU (all 8 workers / ranks share it, so
+      # value and per_gpu_efficiency mean nothing here; the point is the whole path and golden_ok):
+      # the in-process path (mh_search_multi over 8 listed devices) and the launched path (8 ranks)
+      timeout -k 10 600 python "$ROOT/bench.py" --gpus 8 --devices 0,0,0,0,0,0,0,0 --steps 20 --warmup 2 \
+          --no-clock > "$OUT/inproc8_cfg4.json" 2> "$OUT/inproc8_cfg4.err"
+      rc=$?; echo "inproc8 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/inproc8_cfg4.json"; fatal $rc
+      BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+          --master-addr 127.0.0.1 --master-port 29541 "$ROOT/bench.py" --gpus 8 --steps 20 --warmup 2 \
+          --no-clock > "$OUT/dist8_cfg4.json" 2> "$OUT/dist8_cfg4.err"
+      rc=$?; echo "dist8 cfg4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8_cfg4.json"; fatal $rc
+      ;;
     ab:*)
       # an A/B recipe (tools/ab.py, tools/ab/<recipe>.json): one kbench process per workload
       recipe=${s#ab:}
