@@ -22,7 +22,9 @@ shard, merged on the host):
     bench.py --gpus N`): one process per GPU -- the "one miner process per GPU"
     layout of configs[4].  Rank r searches its shard on device LOCAL_RANK with
     mh_search; the tuples, the barrier and the max-over-ranks time go over a
-    gloo (host) process group.  WORLD_SIZE must equal --gpus.
+    gloo (host) process group.  Each step's merge is posted asynchronously and
+    completes while the next step searches (LaunchedSteps); all of them complete
+    inside the timed region.  WORLD_SIZE must equal --gpus.
   * self-contained (`python bench.py --gpus N`, no launcher): one process, one
     host thread + HIP stream per device, mh_search_multi over devices 0..N-1:
     each step is one contiguous shard per device, sized by the device's rate
@@ -147,25 +149,6 @@ def merge(results):
     return min(results)
 
 
-def host_merge_stats(r, world, dist, nonces=0, ns=0):
-    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors), with each
-    rank's (nonces searched, search ns) of the step riding in the same all_gather.
-    Returns (merged tuple, [(nonces, ns) per rank])."""
-    if world == 1:
-        return r, [(nonces, ns)]
-    import torch
-    t = torch.tensor([r[0] - (1 << 63), r[1] - (1 << 63), nonces, ns], dtype=torch.int64)  # u64 -> i64, order kept
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t)
-    vals = [o.tolist() for o in out]
-    return merge((v[0] + (1 << 63), v[1] + (1 << 63)) for v in vals), [(v[2], v[3]) for v in vals]
-
-
-def host_merge(r, world, dist):
-    """The 16-byte tuples of every rank, merged on the host (gloo, CPU tensors)."""
-    return host_merge_stats(r, world, dist)[0]
-
-
 class Balancer:
     """Strong-scaling shard sizes in proportion to each rank's measured search rate.
 
@@ -203,34 +186,86 @@ class Balancer:
         return [max(1, round(self.SCALE * x / top)) for x in rates]
 
 
-def launched_step(search, cfg, rank, world, k, steps, dist, bal=None):
-    """One step of the launched (one process per GPU) path: this rank's shard of step k
-    (rate-weighted when `bal` has rates), searched with search(lo, hi), then the host
-    merge.  Returns (merged (hash, nonce), nonces this rank searched)."""
-    rr = rank_range(cfg, rank, world, k, steps, bal.weights() if bal is not None else None)
-    t0 = time.perf_counter_ns()
-    r = search(rr[0], rr[1]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
-    dt = time.perf_counter_ns() - t0
-    n = rr[1] - rr[0] + 1 if rr else 0
-    merged, stats = host_merge_stats(r, world, dist, n, dt)
-    if bal is not None:
-        bal.update(stats)
-    return merged, n
+class LaunchedSteps:
+    """The steps of the launched (one process per GPU) path, pipelined.  Step k searches this
+    rank's shard of step k (rate-weighted when `bal` has rates) with search(lo, hi) and posts the
+    step's host merge -- the 16-byte tuple and (nonces, search ns) of every rank, one gloo
+    all_gather -- without waiting for it: the merge of step k runs on gloo's thread while step
+    k + 1 searches.  So a rank that finishes a step early starts the next one instead of waiting
+    for the slowest rank, and the merge's latency leaves the critical path; every merge is
+    complete before the timed region ends (finish()).  Step k's shards are sized from the merges
+    of steps <= k - 2, which every rank has folded before cutting step k, so all ranks cut the
+    same shards and the K steps still tile the job exactly once."""
+
+    def __init__(self, search, cfg, rank, world, steps, dist, bal=None):
+        self.search, self.cfg, self.rank, self.world, self.steps = search, cfg, rank, world, steps
+        self.dist, self.bal = dist, bal
+        self.pending = []  # [(k, work, gathered tensors)] in step order
+        self.best = None
+        self.nonces = 0    # this rank's nonces since the last finish()
+
+    def _fold(self, item):
+        k, work, out = item
+        if work is not None:
+            work.wait()
+            vals = [o.tolist() for o in out]
+        else:
+            vals = [out]
+        merged = merge((v[0] + (1 << 63), v[1] + (1 << 63)) for v in vals)
+        self.best = merged if self.best is None else merge([self.best, merged])
+        if self.bal is not None:
+            self.bal.update([(v[2], v[3]) for v in vals])
+
+    def step(self, k):
+        while self.pending and self.pending[0][0] <= k - 2:
+            self._fold(self.pending.pop(0))
+        rr = rank_range(self.cfg, self.rank, self.world, k, self.steps,
+                        self.bal.weights() if self.bal is not None else None)
+        t0 = time.perf_counter_ns()
+        r = self.search(rr[0], rr[1]) if rr else ((1 << 64) - 1, (1 << 64) - 1)
+        dt = time.perf_counter_ns() - t0
+        n = rr[1] - rr[0] + 1 if rr else 0
+        self.nonces += n
+        v = [r[0] - (1 << 63), r[1] - (1 << 63), n, dt]  # u64 -> i64, order kept
+        if self.world == 1:
+            self.pending.append((k, None, v))
+            return
+        import torch
+        t = torch.tensor(v, dtype=torch.int64)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.pending.append((k, self.dist.all_gather(out, t, async_op=True), out))
+
+    def finish(self):
+        """Complete every posted merge; returns the merged (hash, nonce) of the steps since the
+        last finish() and resets it (and the nonce count) for the next region."""
+        while self.pending:
+            self._fold(self.pending.pop(0))
+        best, self.best = self.best, None
+        return best
 
 
-def run_timed(step, steps, warmup, barrier, sync):
+def run_timed(step, steps, warmup, barrier, sync, finish=None):
     """W untimed warmup steps, then exactly `steps` timed steps between a barrier
     + device sync on both sides.  step(k) returns the merged (hash, nonce) of
-    step k.  Returns (min over the timed steps, this rank's elapsed seconds)."""
+    step k, or None when its merge is still in flight: then finish() completes
+    the outstanding merges and returns their minimum (inside the timed region).
+    Returns (min over the timed steps, this rank's elapsed seconds)."""
     for w in range(warmup):
         step(w)
+    if finish is not None:
+        finish()  # the warmup's merges: complete, and not part of the timed result
     barrier()
     sync()
     t0 = time.perf_counter()
     best = None
     for k in range(steps):
         r = step(k)
-        best = r if best is None else merge([best, r])
+        if r is not None:
+            best = r if best is None else merge([best, r])
+    if finish is not None:
+        r = finish()
+        if r is not None:
+            best = r if best is None else merge([best, r])
     barrier()
     sync()
     return best, time.perf_counter() - t0
@@ -761,13 +796,13 @@ def main():
     # strong steps at N > 1: shards in proportion to each rank's measured rate (BENCH_BALANCE=0: equal)
     bal = Balancer(world, cfg["scaling"] == "strong" and os.environ.get("BENCH_BALANCE", "1") != "0")
 
+    pipe = (LaunchedSteps(lambda a, b: minehip.search(msg, a, b, devs[0]), cfg, rank, world, steps, dist, bal)
+            if launched else None)
+
     def step(k, timed=False):
         if launched:
-            r, n = launched_step(lambda a, b: minehip.search(msg, a, b, devs[0]),
-                                 cfg, rank, world, k, steps, dist, bal)
-            if timed:
-                done[devs[0]] += n
-            return r
+            pipe.step(k)  # its host merge completes while the next step searches (LaunchedSteps)
+            return None
         lo, hi = job_range(cfg, n_gpus, k, steps)
         if multi:
             return minehip.search_multi(msg, lo, hi, devs)
@@ -776,6 +811,9 @@ def main():
     barrier = (lambda: dist.barrier()) if launched else (lambda: None)
     for w in range(args.warmup):
         step(w)
+    if launched:
+        pipe.finish()  # the warmup's merges (their rates size the timed shards)
+        pipe.nonces = 0
     n1 = None
     if n_gpus > 1 and not args.no_n1:
         # the same workload on device 0 alone, before the timed region (the other ranks wait)
@@ -784,7 +822,10 @@ def main():
         barrier()
     for d in uniq:
         minehip.profile_enable(d, True)
-    r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize)
+    r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize,
+                           finish=pipe.finish if launched else None)
+    if launched:
+        done[devs[0]] += pipe.nonces
     per_dev = []
     for d in uniq:
         pr = minehip.profile_read(d)
@@ -959,7 +1000,8 @@ def main():
                            "one process, mh_search on one device"),
                 "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
                 "shards": ("each strong step split in proportion to every rank's measured search rate "
-                           "(gathered with the step's merge)" if launched and bal.enabled else
+                           "(gathered with the host merges of the steps before the last, which run while "
+                           "the next step searches)" if launched and bal.enabled else
                            "one shard per device per step, sized by each device's rate measured on the earlier "
                            "steps (mh_search_multi)" if multi else "equal"),
             },

@@ -2,8 +2,9 @@
 
 * The launched path (one process per GPU) over gloo at world 2 and 3: each
   rank scans its shard of every step, the 16-byte (hash, nonce) tuples are
-  merged on the host (gloo all_gather of CPU tensors, no RCCL), and the
-  max-over-ranks time is agreed.  The per-rank search is the oracle here (no
+  merged on the host (gloo all_gather of CPU tensors, no RCCL; each step's
+  merge posted asynchronously and completed while the next step searches,
+  bench.LaunchedSteps), and the max-over-ranks time is agreed.  The per-rank search is the oracle here (no
   GPU); on the box it is minehip.search.
 * Workload tiling: configs[3]'s K strong steps x N shards cover [0, 2^40-1]
   exactly once; weak shards tile [0, N*2^32).
@@ -49,10 +50,8 @@ def _worker(rank, world, port, cfg, steps, q, balance=False, slow_ns=0, warmup=1
             time.sleep((b - a + 1) * slow_ns * (rank + 1) * 1e-9)
         return r
 
-    def step(k):
-        return bench.launched_step(search, cfg, rank, world, k, steps, dist, bal)[0]
-
-    r, elapsed = bench.run_timed(step, steps, warmup, dist.barrier, lambda: None)
+    pipe = bench.LaunchedSteps(search, cfg, rank, world, steps, dist, bal)
+    r, elapsed = bench.run_timed(pipe.step, steps, warmup, dist.barrier, lambda: None, finish=pipe.finish)
     import torch
     t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
