@@ -48,8 +48,8 @@ struct Piece {
 };
 
 struct PlanOpts {
-    // L <= 3 with >= 2^21 runs per bucket and up to 2^34 nonces (~67k workgroups
-    // at L = 3) per launch.  With the issue-priority build the per-run work
+    // L <= 3 (round 2: then with >= 2^21 runs per bucket) and up to 2^34 nonces (~67k
+    // workgroups at L = 3) per launch.  With the issue-priority build the per-run work
     // (digit formatting, hoisted rounds, the first-nonce candidate scan, wave
     // start and the workgroup reduction) costs more than the longer tail of
     // 1,000-nonce lanes: +2% on configs[1], +5% / +4% on configs[2]'s halves,
