@@ -205,7 +205,7 @@ class LaunchedSteps:
         self.nonces = 0    # this rank's nonces since the last finish()
 
     def _fold(self, item):
-        k, work, out = item
+        k, work, out = item[:3]
         if work is not None:
             work.wait()
             vals = [o.tolist() for o in out]
@@ -233,7 +233,8 @@ class LaunchedSteps:
         import torch
         t = torch.tensor(v, dtype=torch.int64)
         out = [torch.empty_like(t) for _ in range(self.world)]
-        self.pending.append((k, self.dist.all_gather(out, t, async_op=True), out))
+        # the input tensor rides along with the outputs: both stay alive until the merge is folded
+        self.pending.append((k, self.dist.all_gather(out, t, async_op=True), out, t))
 
     def finish(self):
         """Complete every posted merge; returns the merged (hash, nonce) of the steps since the
