@@ -555,9 +555,10 @@ def same_workload_n1(search_dev, steps):
     t = time.perf_counter()
     r = search_dev(msg, lo, hi)
     dt = time.perf_counter() - t
+    expect = golden_expect(msg, lo, hi)
     return {"ghs": round((hi - lo + 1) / dt / 1e9, 4), "ms": round(dt * 1e3, 3), "range": [lo, hi],
             "slice": f"step {k} of {k_all}", "result": list(r),
-            "golden_ok": None if golden_expect(msg, lo, hi) is None else tuple(r) == golden_expect(msg, lo, hi)}
+            "golden_ok": None if expect is None else tuple(r) == expect}
 
 
 def per_gpu_efficiency(value, n_gpus, n1_ghs):
