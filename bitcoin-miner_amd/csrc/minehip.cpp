@@ -406,6 +406,7 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
                     uint64_t chunk, uint64_t* out_hash, uint64_t* out_nonce) {
     g_err.clear();
     if (!out_hash || !out_nonce || !devs || ndev <= 0) return fail(MH_EINVAL, "bad arguments");
+    if (ndev > MH_MAX_WORKERS) return fail(MH_EINVAL, "more than MH_MAX_WORKERS devices listed");
     int rc = check_common(msg, len);
     if (rc) return rc;
     if (lower > upper) return fail(MH_ERANGE, "lower > upper");
@@ -641,7 +642,7 @@ int64_t mh_multi_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t u
     int rc = check_common(msg, len);
     if (rc) return rc;
     if (lower > upper) return fail(MH_ERANGE, "lower > upper");
-    if (ndev <= 0 || cap < 0) return fail(MH_EINVAL, "bad arguments");
+    if (ndev <= 0 || ndev > MH_MAX_WORKERS || cap < 0) return fail(MH_EINVAL, "bad arguments");
     std::vector<double> w((size_t)ndev, 1.0);
     if (weights)
         for (int i = 0; i < ndev; ++i) {

@@ -135,7 +135,23 @@ int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, 
         }
     };
     std::vector<std::thread> th;
-    for (int i = 0; i < ndev; ++i) th.emplace_back(worker, i);
+    try {
+        for (int i = 0; i < ndev; ++i) th.emplace_back(worker, i);
+    } catch (...) {
+        // out of threads: the workers that started take the heads of those that did not
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = th.size(); i < (size_t)ndev; ++i)
+            if (!mp.head[i].empty) {
+                queue.push_back(mp.head[i]);
+                --outstanding;
+            }
+        alive -= ndev - (int)th.size();
+        if (!first_err) {
+            first_err = MH_EINTERNAL;
+            err_msg = "could not start a host thread per device";
+        }
+        cv.notify_all();
+    }
     for (auto& t : th) t.join();
     if (!queue.empty() || !any) {
         *err = err_msg.empty() ? "every device failed" : err_msg;

@@ -90,6 +90,10 @@ int mh_search(int dev, const uint8_t *msg, size_t len, uint64_t lower, uint64_t 
 int mh_search_multi(const int *devs, int ndev, const uint8_t *msg, size_t len, uint64_t lower,
                     uint64_t upper, uint64_t chunk, uint64_t *out_hash, uint64_t *out_nonce);
 
+/* Most entries a device list of mh_search_multi / mh_multi_plan may have (one host thread each;
+ * a device may be listed more than once). */
+#define MH_MAX_WORKERS 256
+
 /* out_hashes[i] = Hash(msg, nonces[i]) computed on device `dev` -- the batched
  * GPU form of bitcoin.Hash (hash.go:13-17).  n may be 0. */
 int mh_hash_batch(int dev, const uint8_t *msg, size_t len, const uint64_t *nonces, size_t n,

@@ -91,6 +91,10 @@ def test_split_argument_errors():
     with pytest.raises(minehip.MinehipError) as e:
         minehip.multi_plan(b"x", 0, 4, 0)
     assert e.value.code == minehip.MH_EINVAL
+    with pytest.raises(minehip.MinehipError) as e:  # one host thread per listed device: bounded
+        minehip.multi_plan(b"x", 0, 4, minehip._lib.MH_MAX_WORKERS + 1)
+    assert e.value.code == minehip.MH_EINVAL
+    assert len(minehip.multi_plan(b"x", 0, 10 ** 6, minehip._lib.MH_MAX_WORKERS)) == minehip._lib.MH_MAX_WORKERS
 
 
 def test_rate_table_starts_empty():
