@@ -83,8 +83,11 @@ struct DevCtx {
     int dev = -1;
     bool ready = false;
     hipStream_t stream = nullptr;              // every search's merge and copy; pieces with streams = 1
-    hipStream_t s_hi = nullptr, s_lo = nullptr;  // streams = 2: coarse / fine pieces (priorities)
-    hipEvent_t ev_join[3] = {nullptr, nullptr, nullptr};
+    // streams = 2: the pieces' streams, by priority: [0] coarse pieces (highest), [1] the other pieces
+    // when a finest tail is planned (normal), [2] the other pieces, or the finest tail (lowest)
+    hipStream_t ps[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_piece[3] = {nullptr, nullptr, nullptr};  // each piece stream's work so far
+    hipEvent_t ev_main = nullptr;                          // the main stream's (reset / merge)
     Partial* d_partials = nullptr;
     Partial* d_best = nullptr;
     Partial* h_best = nullptr;  // pinned
@@ -137,14 +140,16 @@ int init_locked(DevCtx* c, int dev) {
     // each resource only once: a call after a failed init (e.g. the code object
     // did not load) resumes where that one stopped instead of allocating again
     if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (!c->s_hi || !c->s_lo) {
+    if (!c->ps[0] || !c->ps[1] || !c->ps[2]) {
         int least = 0, greatest = 0;
-        MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        if (!c->s_hi) MH_HIP(hipStreamCreateWithPriority(&c->s_hi, hipStreamNonBlocking, greatest));
-        if (!c->s_lo) MH_HIP(hipStreamCreateWithPriority(&c->s_lo, hipStreamNonBlocking, least));
+        MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));  // gfx950: 1 .. -1
+        const int prio[3] = {greatest, (least + greatest) / 2, least};
+        for (int k = 0; k < 3; ++k)
+            if (!c->ps[k]) MH_HIP(hipStreamCreateWithPriority(&c->ps[k], hipStreamNonBlocking, prio[k]));
     }
-    for (auto& e : c->ev_join)
+    for (auto& e : c->ev_piece)
         if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->ev_main) MH_HIP(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
     if (!c->d_partials) MH_HIP(hipMalloc(&c->d_partials, sizeof(Partial) * mh::kMaxBlocksPerLaunch));
     if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
     if (!c->d_counters) MH_HIP(hipMalloc(&c->d_counters, sizeof(uint32_t) * kQueueSlots));
@@ -178,21 +183,24 @@ int harvest_locked(DevCtx* c) {
 // Fold the pending partials into the running minimum.  With two piece
 // streams the merge (on the main stream) first waits for both, and both wait
 // for the merge before any later piece reuses the partials buffer.
+// The piece streams start after the main stream's work so far (the reset, a merge).
+int piece_streams_wait_main(DevCtx* c) {
+    MH_HIP(hipEventRecord(c->ev_main, c->stream));
+    for (auto s : c->ps) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
+    return MH_OK;
+}
+
 int flush_partials(DevCtx* c, bool split) {
     if (!c->poff) return MH_OK;
     if (split) {
-        MH_HIP(hipEventRecord(c->ev_join[0], c->s_hi));
-        MH_HIP(hipEventRecord(c->ev_join[1], c->s_lo));
-        MH_HIP(hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
-        MH_HIP(hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
+        for (int k = 0; k < 3; ++k) {
+            MH_HIP(hipEventRecord(c->ev_piece[k], c->ps[k]));
+            MH_HIP(hipStreamWaitEvent(c->stream, c->ev_piece[k], 0));
+        }
     }
     MH_HIP(mh::launch_merge(c->d_partials, c->poff, c->d_best, c->stream));
     c->poff = 0;
-    if (split) {
-        MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
-        MH_HIP(hipStreamWaitEvent(c->s_hi, c->ev_join[2], 0));
-        MH_HIP(hipStreamWaitEvent(c->s_lo, c->ev_join[2], 0));
-    }
+    if (split) return piece_streams_wait_main(c);
     return MH_OK;
 }
 
@@ -203,9 +211,18 @@ bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) {
     return p.kind == 0 && p.L == opt.lower_digits && p.count >= opt.coarse_min;
 }
 
+// The piece stream of p (streams = 2): coarse pieces on the highest priority; the finest tail, when
+// planned, on the lowest, below every other piece (normal priority then), so that it is dispatched
+// last and its short workgroups fill the drain of the search's last pieces.
+hipStream_t piece_stream(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
+    if (coarse_piece(p, opt)) return c->ps[0];
+    if (p.finest) return c->ps[2];
+    return opt.finest_tail ? c->ps[1] : c->ps[2];
+}
+
 int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
     // split: coarse pieces (the full L) on the high-priority stream, the rest on the low one
-    hipStream_t s = !split ? c->stream : coarse_piece(p, opt) ? c->s_hi : c->s_lo;
+    hipStream_t s = !split ? c->stream : piece_stream(c, p, opt);
     uint32_t blocks;
     if (p.kind == 0) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
@@ -234,8 +251,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
-            MH_HIP(hipStreamSynchronize(c->s_hi));
-            MH_HIP(hipStreamSynchronize(c->s_lo));
+            for (auto ps : c->ps) MH_HIP(hipStreamSynchronize(ps));
             int rc = harvest_locked(c);
             if (rc) return rc;
         }
@@ -282,6 +298,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
 //                          XCDs take more; default); 0: one workgroup per chunk
 //   MINEHIP_COARSE_MIN     full-L pieces smaller than this go to the low-priority stream (0)
+//   MINEHIP_FINEST_TAIL    nonces at the end of each tail split planned at L - 2, on the lowest-
+//                          priority stream (0: none)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -308,6 +326,7 @@ mh::PlanOpts plan_opts() {
         if (v == 0 || v == 1) o.queue = v;
     }
     if (const char* e = getenv("MINEHIP_COARSE_MIN")) o.coarse_min = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("MINEHIP_FINEST_TAIL")) o.finest_tail = strtoull(e, nullptr, 10);
     return o;
 }
 
@@ -344,10 +363,9 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
             return !(any_coarse && any_fine);
         });
     const bool split = opt.streams == 2 && any_coarse && any_fine;
-    if (split) {  // both piece streams start after the reset (and after the previous search)
-        MH_HIP(hipEventRecord(c->ev_join[2], c->stream));
-        MH_HIP(hipStreamWaitEvent(c->s_hi, c->ev_join[2], 0));
-        MH_HIP(hipStreamWaitEvent(c->s_lo, c->ev_join[2], 0));
+    if (split) {  // the piece streams start after the reset (and after the previous search)
+        rc = piece_streams_wait_main(c);
+        if (rc) return rc;
     }
     int err = MH_OK;
     c->poff = 0;
@@ -357,8 +375,7 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     });
     if (!err) err = flush_partials(c, split);
     if (err) {
-        (void)hipStreamSynchronize(c->s_hi);
-        (void)hipStreamSynchronize(c->s_lo);
+        for (auto ps : c->ps) (void)hipStreamSynchronize(ps);
         (void)hipStreamSynchronize(c->stream);
         return err;
     }

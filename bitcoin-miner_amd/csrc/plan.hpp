@@ -43,6 +43,7 @@ struct Piece {
     int blocks;       // tail blocks of the final message
     uint32_t ops;     // fast only: nonce_cost(J, mode).ops
     uint32_t slots;   // fast only: nonce_cost(J, mode).slots
+    int finest;       // fast only: 1 for the finest tail of a bucket (PlanOpts.finest_tail)
     FastArgs fa;      // kind 0
     GenArgs ga;       // both (generic launch args; also used by hash_batch)
 };
@@ -86,6 +87,10 @@ struct PlanOpts {
     // Execution: a full-L piece goes to the high-priority stream only if it has at least coarse_min
     // nonces (smaller ones back-fill from the low-priority stream).  0: every full-L piece.
     uint64_t coarse_min = 0;
+    // Finest tail (experiment, 0: off): the last finest_tail nonces of each tail split planned once
+    // more at L - 2, marked `finest` and run on the lowest-priority stream, the other non-coarse
+    // pieces then on a normal-priority one, so the search ends on 10-nonce lanes.
+    uint64_t finest_tail = 0;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

@@ -164,6 +164,17 @@ def test_plan_fine_tail_covers_exactly(monkeypatch):
         check_plan(m, U64 - (1 << 33), U64)
 
 
+def test_plan_finest_tail_covers_exactly(monkeypatch):
+    """MINEHIP_FINEST_TAIL (experiment): the last runs of each tail split planned once more at L - 2;
+    the plan still tiles the range exactly."""
+    monkeypatch.setenv("MINEHIP_FINEST_TAIL", str(1 << 25))
+    for m in (b"cmu440", b"x" * 60, b"a" * 100, b"y" * 52):
+        pieces = check_plan(m, 0, 2 ** 34 - 1)
+        assert [p for p in pieces if p["kind"] == 0 and p["lo_digits"] == 1 and p["count"] <= 1 << 25]
+        check_plan(m, 549755813888, 549755813888 + 6871947673)
+        check_plan(m, U64 - (1 << 33), U64)
+
+
 def test_plan_uses_fast_kernel_for_bulk():
     pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
     fast = sum(p["count"] for p in pieces if p["kind"] == 0)

@@ -176,6 +176,11 @@ def test_plan_invariance_small(gpu):
                                  MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
                                  MINEHIP_QUEUE=q):
                             assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st, ft, q)
+        # the finest tail on the lowest-priority stream (MINEHIP_FINEST_TAIL)
+        for ft in (1_000, 50_000):
+            with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
+                     MINEHIP_STREAMS=2, MINEHIP_FINE_TAIL=200_000, MINEHIP_FINEST_TAIL=ft):
+                assert gpu.search(m, lo, hi) == exp, (m[:8], ft)
         # which full-L pieces take the high-priority stream (MINEHIP_COARSE_MIN)
         for cm in (1, 100_000, 1 << 62):
             with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
