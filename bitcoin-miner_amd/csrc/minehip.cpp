@@ -140,12 +140,11 @@ int init_locked(DevCtx* c, int dev) {
     // each resource only once: a call after a failed init (e.g. the code object
     // did not load) resumes where that one stopped instead of allocating again
     if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (!c->ps[0] || !c->ps[1] || !c->ps[2]) {
+    if (!c->ps[0] || !c->ps[2]) {  // ps[1] only once a search plans a finest tail (ensure_mid_stream)
         int least = 0, greatest = 0;
         MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));  // gfx950: 1 .. -1
-        const int prio[3] = {greatest, (least + greatest) / 2, least};
-        for (int k = 0; k < 3; ++k)
-            if (!c->ps[k]) MH_HIP(hipStreamCreateWithPriority(&c->ps[k], hipStreamNonBlocking, prio[k]));
+        if (!c->ps[0]) MH_HIP(hipStreamCreateWithPriority(&c->ps[0], hipStreamNonBlocking, greatest));
+        if (!c->ps[2]) MH_HIP(hipStreamCreateWithPriority(&c->ps[2], hipStreamNonBlocking, least));
     }
     for (auto& e : c->ev_piece)
         if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -183,10 +182,20 @@ int harvest_locked(DevCtx* c) {
 // Fold the pending partials into the running minimum.  With two piece
 // streams the merge (on the main stream) first waits for both, and both wait
 // for the merge before any later piece reuses the partials buffer.
+// The normal-priority piece stream, created when a search first plans a finest tail.
+int ensure_mid_stream(DevCtx* c) {
+    if (c->ps[1]) return MH_OK;
+    int least = 0, greatest = 0;
+    MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    MH_HIP(hipStreamCreateWithPriority(&c->ps[1], hipStreamNonBlocking, (least + greatest) / 2));
+    return MH_OK;
+}
+
 // The piece streams start after the main stream's work so far (the reset, a merge).
 int piece_streams_wait_main(DevCtx* c) {
     MH_HIP(hipEventRecord(c->ev_main, c->stream));
-    for (auto s : c->ps) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
+    for (auto s : c->ps)
+        if (s) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
     return MH_OK;
 }
 
@@ -194,6 +203,7 @@ int flush_partials(DevCtx* c, bool split) {
     if (!c->poff) return MH_OK;
     if (split) {
         for (int k = 0; k < 3; ++k) {
+            if (!c->ps[k]) continue;
             MH_HIP(hipEventRecord(c->ev_piece[k], c->ps[k]));
             MH_HIP(hipStreamWaitEvent(c->stream, c->ev_piece[k], 0));
         }
@@ -251,7 +261,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
-            for (auto ps : c->ps) MH_HIP(hipStreamSynchronize(ps));
+            for (auto ps : c->ps)
+                if (ps) MH_HIP(hipStreamSynchronize(ps));
             int rc = harvest_locked(c);
             if (rc) return rc;
         }
@@ -364,6 +375,10 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
         });
     const bool split = opt.streams == 2 && any_coarse && any_fine;
     if (split) {  // the piece streams start after the reset (and after the previous search)
+        if (opt.finest_tail) {
+            rc = ensure_mid_stream(c);
+            if (rc) return rc;
+        }
         rc = piece_streams_wait_main(c);
         if (rc) return rc;
     }
@@ -375,7 +390,8 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     });
     if (!err) err = flush_partials(c, split);
     if (err) {
-        for (auto ps : c->ps) (void)hipStreamSynchronize(ps);
+        for (auto ps : c->ps)
+            if (ps) (void)hipStreamSynchronize(ps);
         (void)hipStreamSynchronize(c->stream);
         return err;
     }
