@@ -101,7 +101,10 @@ int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, 
                 uint64_t h = 0, nn = 0, ns = 0;
                 std::string e;
                 const int r = search(i, devs[i], cur.lo, cur.hi, &h, &nn, &ns, &e);
-                if (r == MH_OK && cur.hi - cur.lo >= kRateMinNonces - 1u)
+                // a device's rate comes from long spans of steady buckets only: a shard holding the
+                // small buckets of a range would otherwise read as a slower device (multi.hpp)
+                if (r == MH_OK && cur.hi - cur.lo >= kRateMinNonces - 1u &&
+                    unsteady_share(mp.segs, cur.lo, cur.hi) < kRateMaxUnsteady)
                     record_rate(devs[i], segments_cost(mp.segs, cur.lo, cur.hi), ns);
                 std::lock_guard<std::mutex> lk(mu);
                 --outstanding;

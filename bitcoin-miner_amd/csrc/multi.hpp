@@ -25,6 +25,7 @@ namespace mh {
 constexpr uint64_t kTailMinPerWorker = 1ull << 35;  // nonces per worker before a dynamic tail is cut
 constexpr int kTailDiv = 16;                         // the tail is 1/kTailDiv of the cost
 constexpr uint64_t kRateMinNonces = 1ull << 30;      // shorter searches are latency, not rate
+constexpr double kRateMaxUnsteady = 0.01;            // ... and spans of small buckets are off the model
 
 struct MultiPlan {
     std::vector<CostSeg> segs;

@@ -246,7 +246,9 @@ void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const Plan
         int L = 0, J = 0, mode = 0, nb = 1;
         FastArgs fa;
         double per;
+        bool steady = false;
         if (bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &fa)) {
+            steady = L == opt.lower_digits && (B - A) / kPow10[L] + 1u >= (1u << 21);
             // the fast kernel's issue slots per nonce, plus the per-run / per-group work that shorter
             // lanes amortise over fewer nonces (L = 2: ~3%, L = 1: ~6% per nonce)
             per = (double)nonce_cost(J, mode).slots * (1.0 + 0.03 * (double)(3 - std::min(L, 3)));
@@ -255,8 +257,20 @@ void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const Plan
             const int blocks = (pre.t + (uint32_t)d + 9u <= 64u) ? 1 : 2;
             per = (double)kGenericSlotsPerBlock * blocks;
         }
-        out->push_back(CostSeg{A, B, per});
+        out->push_back(CostSeg{A, B, per, steady});
     }
+}
+
+double unsteady_share(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi) {
+    double all = 0.0, unsteady = 0.0;
+    for (const CostSeg& s : segs) {
+        const uint64_t a = std::max(s.a, lo), b = std::min(s.b, hi);
+        if (a > b) continue;
+        const double c = ((double)(b - a) + 1.0) * s.per;
+        all += c;
+        if (!s.steady) unsteady += c;
+    }
+    return all > 0.0 ? unsteady / all : 0.0;
 }
 
 double segments_cost(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi) {

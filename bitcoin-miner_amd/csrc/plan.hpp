@@ -127,7 +127,13 @@ int decimal_digits(uint64_t n);
 struct CostSeg {
     uint64_t a, b;  // inclusive
     double per;
+    // the bucket runs at the full L in a launch of many generations of workgroups (>= 2^21 runs):
+    // its time follows `per`; the shorter-lane, few-generation and generic buckets run a few to
+    // ~20% off the model (drains), so a device's rate is only measured on steady spans
+    bool steady;
 };
+// Share of [lo, hi]'s cost in segments that are not steady.
+double unsteady_share(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi);
 constexpr double kGenericSlotsPerBlock = 2.0 * 1760.0;  // estimate: a full compression + per-nonce formatting
 void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
                    std::vector<CostSeg>* out);
