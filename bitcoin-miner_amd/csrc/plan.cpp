@@ -252,6 +252,10 @@ void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const Plan
             // the fast kernel's issue slots per nonce, plus the per-run / per-group work that shorter
             // lanes amortise over fewer nonces (L = 2: ~3%, L = 1: ~6% per nonce)
             per = (double)nonce_cost(J, mode).slots * (1.0 + 0.03 * (double)(3 - std::min(L, 3)));
+            // a bucket of few generations of workgroups ends in a drain only partly back-filled:
+            // the one-GPU model measured configs[3]'s d = 7..9 buckets in an 8-GPU shard ~15-20%
+            // over the steady rate (profiles/r04o_inproc_model.json)
+            if (!steady) per *= kUnsteadyFactor;
         } else {
             // generic kernel: every nonce formatted and hashed from the midstate
             const int blocks = (pre.t + (uint32_t)d + 9u <= 64u) ? 1 : 2;

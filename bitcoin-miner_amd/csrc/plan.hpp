@@ -135,6 +135,7 @@ struct CostSeg {
 // Share of [lo, hi]'s cost in segments that are not steady.
 double unsteady_share(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi);
 constexpr double kGenericSlotsPerBlock = 2.0 * 1760.0;  // estimate: a full compression + per-nonce formatting
+constexpr double kUnsteadyFactor = 1.15;                 // fast buckets that are not steady (below)
 void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpts& opt,
                    std::vector<CostSeg>* out);
 double segments_cost(const std::vector<CostSeg>& segs, uint64_t lo, uint64_t hi);
