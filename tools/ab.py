@@ -34,6 +34,8 @@ WORKLOADS = {
     "cfg4slice": ("cmu440", 1 << 39, 1 << 36),            # a 2^36 slice of configs[3]
     "cfg4step": ("cmu440", 1 << 39, (1 << 40) // 20),     # one of configs[3]'s 20 bench steps
     "shard8": ("cmu440", 1 << 39, 6871947673),            # one 8-GPU shard of a configs[3] step
+    "shard4": ("cmu440", 1 << 39, 13743895347),           # one 4-GPU shard
+    "shard2": ("cmu440", 1 << 39, 27487790694),           # one 2-GPU shard
     "p55": (("cmu440-" * 10)[:55], 0, 1 << 32),           # <13|14|15, Two> layouts
 }
 FATAL = {124, 134, 137, 139}
