@@ -63,7 +63,12 @@ struct PlanOpts {
     // lanes), configs[2] +0.4% / +0.6%; 2^16 (buckets of a fifth of a generation at L = 3) -4.7%
     // (profiles/r04c_kbench_min_lanes_*.json).
     uint64_t min_lanes = 1u << 19;
-    uint64_t max_nonces_per_launch = 1ull << 34; // one launch <= ~0.35 s (one tail block) / ~0.6 s (two)
+    // Nonces per fast launch: 2^35, so with the 2^17-workgroup cap one launch takes up to ~3.4e10
+    // nonces at L = 3 (~0.6 s with one tail block).  A bucket's launches run back to back on the
+    // high-priority stream and every boundary drains; round 4 against 2^34, A/B in one process: a
+    // configs[3] step (5.5e10 nonces, 2 launches instead of 4) +0.52% / +0.58% on two boxes, a
+    // 2-GPU shard +0.41%, configs[1] and [2] unchanged plans (profiles/r04r_kbench_launch_size_*.json).
+    uint64_t max_nonces_per_launch = 1ull << 35;
     uint32_t max_blocks = 1u << 17;              // workgroups per launch (<= kMaxBlocksPerLaunch; +0.1% over 2^16)
     uint64_t generic_below = 1u << 20;           // a bucket this small goes to the generic kernel whole
     // Execution (minehip.cpp, not the plan itself): 1 = every piece on one stream in nonce

@@ -197,19 +197,19 @@ def test_plan_coalesces_small_buckets():
 
 
 def test_plan_launch_cap():
-    """PlanOpts: at most 2^34 nonces and 131,072 workgroups of 256 lanes per fast launch, and
-    configs[3]'s big buckets run 1,000-nonce lanes (L = 3) in launches near the nonce cap, each
+    """PlanOpts: at most 2^35 nonces and 131,072 workgroups of 256 lanes per fast launch, and
+    configs[3]'s big buckets run 1,000-nonce lanes (L = 3) in launches near the cap, each
     bucket ending in one tail piece of <= 2^28 nonces at L = 2 (the default fine_tail)."""
     pieces = check_plan(b"cmu440", 0, 2 ** 40 - 1)
     fast = [p for p in pieces if p["kind"] == 0]
-    assert max(p["count"] for p in pieces) <= 2 ** 34
+    assert max(p["count"] for p in pieces) <= 2 ** 35
     for p in fast:
         assert -(-(p["count"] // 10 ** p["lo_digits"]) // 256) <= 131072
     for d in (11, 12, 13):
         b = [p for p in fast if p["digits"] == d]
         assert [p["lo_digits"] for p in b] == [3] * (len(b) - 1) + [2]
         assert b[-1]["count"] <= 2 ** 28 and b[-1]["count"] > 2 ** 27
-        assert max(p["count"] for p in b) > 2 ** 33
+        assert max(p["count"] for p in b) > 2 ** 34
 
 
 # ---- bitcoin.Message codec (Go encoding/json bytes) ------------------------
