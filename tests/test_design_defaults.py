@@ -1,0 +1,34 @@
+"""DESIGN.md §3's table of shipped plan defaults matches PlanOpts in csrc/plan.hpp (VERDICT r03
+next-round item 5: the document states the defaults the code ships)."""
+import os
+import re
+
+from conftest import ROOT
+
+
+def plan_defaults():
+    src = open(os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "plan.hpp")).read()
+    body = src[src.index("struct PlanOpts"):]
+    body = body[:body.index("\n};")]
+    out = {}
+    for name, val in re.findall(r"^\s*(?:int|uint64_t|uint32_t)\s+(\w+)\s*=\s*([^;]+);", body, flags=re.M):
+        val = val.strip()
+        m = re.fullmatch(r"1u?l?l?\s*<<\s*(\d+)", val)
+        out[name] = f"2^{m.group(1)}" if m else val
+    return out
+
+
+def design_table():
+    doc = open(os.path.join(ROOT, "DESIGN.md")).read()
+    sec = doc[doc.index("**Shipped defaults**"):doc.index("**Two streams.**")]
+    out = {}
+    for row in re.findall(r"^\| `(\w+)`[^|]*\| \*\*([^*]+)\*\*", sec, flags=re.M):
+        out[row[0]] = row[1].split(":")[0].strip()
+    return out
+
+
+def test_design_states_the_shipped_defaults():
+    code, doc = plan_defaults(), design_table()
+    assert set(code) == set(doc), (sorted(code), sorted(doc))
+    for k, v in code.items():
+        assert doc[k] == v, (k, doc[k], v)
