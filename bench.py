@@ -540,6 +540,25 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
                     "fast_search<4, One> (tools/clock_probe.hip)"}
 
 
+def rank_device(local, ndev):
+    """The HIP device of a launched rank: LOCAL_RANK when the process sees every GPU of the node,
+    device 0 when the launcher gives each rank exactly one visible GPU (HIP/ROCR_VISIBLE_DEVICES
+    per rank), None when LOCAL_RANK names no visible device."""
+    if 0 <= local < ndev:
+        return local
+    if ndev == 1 and local >= 0:
+        return 0
+    return None
+
+
+def ranks_per_device(idents):
+    """The most ranks any one GPU serves, from every rank's device identity (PCI domain, bus,
+    device): 1 on a node with a GPU per rank; more means the ranks share a card and per-GPU
+    figures are not per-GPU (the one-GPU rehearsals set BENCH_DEVICE and expect it)."""
+    from collections import Counter
+    return max(Counter(tuple(i) for i in idents).values()) if idents else 0
+
+
 def same_workload_n1(search_dev, steps):
     """One step of the scaling workload on ONE device: BASELINE configs[3]'s middle slice
     ("cmu440", 2^40 / K nonces with K = max(steps, 20): the driver's --steps 20 step) searched
@@ -768,9 +787,10 @@ def main():
     import torch
     ndev = torch.cuda.device_count()
     if launched:
-        if local >= ndev:
+        d = rank_device(local, ndev)
+        if d is None:
             die(f"rank {rank}: HIP device {local} not visible ({ndev} visible)")
-        devs = [local]
+        devs = [d]
     elif args.devices:
         devs = [int(x) for x in args.devices.split(",")]
         if len(devs) != args.gpus or any(d < 0 or d >= ndev for d in devs):
@@ -784,9 +804,17 @@ def main():
     if minehip.device_count() != ndev:
         die(f"libminehip sees {minehip.device_count()} devices, torch {ndev}")
     dist = None
+    shared = None
     if launched:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)  # host merge: no RCCL
+        pr = torch.cuda.get_device_properties(devs[0])
+        idents = [None] * world
+        dist.all_gather_object(idents, (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
+        shared = ranks_per_device(idents)
+        if shared > 1 and os.environ.get("BENCH_DEVICE") is None and rank == 0:
+            print(f"bench: {shared} ranks share one GPU (device visibility); per-GPU figures are not per GPU",
+                  file=sys.stderr)
 
     msg = cfg["msg"].encode()
     n_gpus = args.gpus
@@ -1001,6 +1029,8 @@ def main():
                            "one process, mh_search_multi: one host thread + HIP stream per device" if multi else
                            "one process, mh_search on one device"),
                 "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
+                # launched: the most ranks one physical GPU served (1 = one GPU per rank)
+                "ranks_per_device": shared if launched else None,
                 "shards": ("each strong step split in proportion to every rank's measured search rate "
                            "(gathered with the host merges of the steps before the last, which run while "
                            "the next step searches)" if launched and bal.enabled else

@@ -235,6 +235,20 @@ def test_world_size_mismatch_exits_without_json():
     assert _json_lines(p.stdout) == []
 
 
+def test_rank_device_and_sharing():
+    """A launched rank runs on LOCAL_RANK when it sees the node's GPUs, on device 0 when the
+    launcher isolates one GPU per rank, and refuses a LOCAL_RANK naming no device; the line's
+    ranks_per_device counts ranks per physical GPU (PCI identity)."""
+    assert bench.rank_device(3, 8) == 3
+    assert bench.rank_device(0, 8) == 0
+    assert bench.rank_device(5, 1) == 0    # HIP/ROCR_VISIBLE_DEVICES per rank
+    assert bench.rank_device(5, 4) is None
+    assert bench.rank_device(0, 0) is None
+    assert bench.ranks_per_device([(0, 0x11, 0), (0, 0x21, 0), (0, 0x31, 0)]) == 1
+    assert bench.ranks_per_device([(0, 0x11, 0)] * 8) == 8     # the one-GPU rehearsal
+    assert bench.ranks_per_device([(0, 0x11, 0), (0, 0x11, 0), (0, 0x21, 0)]) == 2
+
+
 def test_same_workload_n1_slice_and_efficiency():
     """Every line's n1_config4_ghs is one configs[3] step -- the middle 2^40/20 slice the driver's
     --steps 20 line runs -- searched on one device; per_gpu_efficiency = value / (N x it)

@@ -168,6 +168,12 @@ for s in $STEPS; do
           --master-addr 127.0.0.1 --master-port 29533 "$ROOT/bench.py" --gpus 2 --steps 4 --warmup 1 \
           --bits 36 > "$OUT/dist2.json" 2> "$OUT/dist2.err"
       rc=$?; echo "dist2 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist2.json"; fatal $rc
+      # the same with one GPU visible per rank (a launcher isolating ranks): LOCAL_RANK 1 runs on
+      # its only visible device, and the line says two ranks shared it
+      HIP_VISIBLE_DEVICES=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29536 "$ROOT/bench.py" --gpus 2 --steps 4 --warmup 1 \
+          --bits 36 > "$OUT/dist2_vis.json" 2> "$OUT/dist2_vis.err"
+      rc=$?; echo "dist2 per-rank visibility rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist2_vis.json"; fatal $rc
       ;;
     dist8)
       # 8 ranks on the box's one GPU: bench.py's N = 8 sharding and host merge (2^36, golden-checked weak line too)
