@@ -30,6 +30,7 @@
 namespace mh {
 hipError_t fast_module_init(int dev);
 hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, hipStream_t s);
+hipError_t fast_queue_ok(int dev, int J, int mode, bool* ok);
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
                              hipStream_t s);
@@ -64,6 +65,7 @@ namespace {
 constexpr uint64_t kBatchChunk = 1u << 22;  // nonces per hash_batch transfer
 constexpr int kEventPairs = 512;             // profiled launches buffered before harvesting
 constexpr uint32_t kQueueSlots = 4096;       // work-queue counters per search (one per fast launch)
+constexpr uint32_t kNextSlots = 256;         // fused-tail argument blocks per search (one per fused launch)
 
 struct Timed {
     hipEvent_t start = nullptr, stop = nullptr;
@@ -96,6 +98,9 @@ struct DevCtx {
     uint32_t poff = 0;  // partials written since the last merge
     uint32_t* d_counters = nullptr;  // work-queue counters, zeroed at each search's start
     uint32_t qoff = 0;               // counters used by this search
+    mh::FastArgs* d_next = nullptr;  // fused tails' arguments (device), staged through
+    mh::FastArgs* h_next = nullptr;  // ... pinned host slots; one per fused launch of a search
+    uint32_t noff = 0;               // slots used by this search
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
@@ -153,6 +158,8 @@ int init_locked(DevCtx* c, int dev) {
     if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
     if (!c->d_counters) MH_HIP(hipMalloc(&c->d_counters, sizeof(uint32_t) * kQueueSlots));
     if (!c->h_best) MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
+    if (!c->d_next) MH_HIP(hipMalloc(&c->d_next, sizeof(mh::FastArgs) * kNextSlots));
+    if (!c->h_next) MH_HIP(hipHostMalloc(&c->h_next, sizeof(mh::FastArgs) * kNextSlots, hipHostMallocDefault));
     if (!c->d_nonces) MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
     if (!c->d_hashes) MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
     if (c->pool.empty()) c->pool.resize(kEventPairs);
@@ -230,7 +237,10 @@ hipStream_t piece_stream(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt)
     return opt.finest_tail ? c->ps[1] : c->ps[2];
 }
 
-int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
+// tail (optional): the bucket's tail split, fused into p's launch (PlanOpts.fuse_tail; the caller
+// checked fusable()).
+int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split,
+                  const mh::Piece* tail = nullptr) {
     // split: coarse pieces (the full L) on the high-priority stream, the rest on the low one
     hipStream_t s = !split ? c->stream : piece_stream(c, p, opt);
     uint32_t blocks;
@@ -245,8 +255,15 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
             return fail(MH_EINTERNAL, "internal: bad generic piece");
         blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
     }
-    if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
-    if (c->poff + blocks > mh::kMaxBlocksPerLaunch) {
+    uint32_t tail_blocks = 0;
+    if (tail) {
+        if (tail->kind != 0 || tail->fa.n_runs == 0 || tail->fa.L < 1 || tail->fa.n_hi + tail->fa.L > 20 ||
+            tail->J != p.J || tail->mode != p.mode)
+            return fail(MH_EINTERNAL, "internal: bad fused tail");
+        tail_blocks = (tail->fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
+    }
+    if (blocks + tail_blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
+    if (c->poff + blocks + tail_blocks > mh::kMaxBlocksPerLaunch) {
         const int rc = flush_partials(c, split);
         if (rc) return rc;
     }
@@ -257,6 +274,21 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
         fa.n_chunks = blocks;
         // work queue while this search has counters left (a longer search runs the rest static)
         fa.counter = (opt.queue && c->qoff < kQueueSlots) ? c->d_counters + c->qoff++ : nullptr;
+        fa.next = nullptr;
+        fa.next_chunks = 0;
+        if (tail) {
+            if (!fa.counter || c->noff >= kNextSlots) return fail(MH_EINTERNAL, "internal: no slot for a fused tail");
+            mh::FastArgs* h = c->h_next + c->noff;
+            *h = tail->fa;
+            h->n_chunks = tail_blocks;
+            h->counter = nullptr;
+            h->next = nullptr;
+            h->next_chunks = 0;
+            fa.next = c->d_next + c->noff++;
+            fa.next_chunks = tail_blocks;
+            // stream-ordered before the launch; the slot is not rewritten before the search's end sync
+            MH_HIP(hipMemcpyAsync((void*)fa.next, h, sizeof(mh::FastArgs), hipMemcpyHostToDevice, s));
+        }
     }
     if (c->prof) {
         if (c->used == kEventPairs) {
@@ -276,18 +308,20 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     else
         MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, s));
     if (tm) MH_HIP(hipEventRecord(tm->stop, s));
-    c->poff += blocks;
+    c->poff += blocks + tail_blocks;
     if (c->prof) {
         if (p.kind == 0) {
+            // a fused tail's nonces count with the launch they ran in (same kernel, same nonce_ops)
+            const uint64_t n = p.count + (tail ? tail->count : 0u);
             c->cnt[0] += 1;
-            c->cnt[1] += p.count;
-            c->cnt[3] += p.count * (uint64_t)p.ops;
-            c->cnt[6] += p.count * (uint64_t)p.slots;
+            c->cnt[1] += n;
+            c->cnt[3] += n * (uint64_t)p.ops;
+            c->cnt[6] += n * (uint64_t)p.slots;
             VarStat& v = c->var[var_index(p.J, p.mode, p.L)];
             v.launches += 1;
-            v.nonces += p.count;
-            v.ops += p.count * (uint64_t)p.ops;
-            v.slots += p.count * (uint64_t)p.slots;
+            v.nonces += n;
+            v.ops += n * (uint64_t)p.ops;
+            v.slots += n * (uint64_t)p.slots;
         } else {
             c->cnt[4] += p.count;
         }
@@ -311,6 +345,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //   MINEHIP_COARSE_MIN     full-L pieces smaller than this go to the low-priority stream (0)
 //   MINEHIP_FINEST_TAIL    nonces at the end of each tail split planned at L - 2, on the lowest-
 //                          priority stream (0: none)
+//   MINEHIP_FUSE_TAIL      1: each tail split runs as the last chunks of the coarse launch before
+//                          it (work queue only); 0: a launch of its own (default)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -338,6 +374,10 @@ mh::PlanOpts plan_opts() {
     }
     if (const char* e = getenv("MINEHIP_COARSE_MIN")) o.coarse_min = strtoull(e, nullptr, 10);
     if (const char* e = getenv("MINEHIP_FINEST_TAIL")) o.finest_tail = strtoull(e, nullptr, 10);
+    if (const char* e = getenv("MINEHIP_FUSE_TAIL")) {
+        const int v = atoi(e);
+        if (v == 0 || v == 1) o.fuse_tail = v;
+    }
     return o;
 }
 
@@ -384,10 +424,37 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     }
     int err = MH_OK;
     c->poff = 0;
+    c->noff = 0;
+    // Fused tails (opt.fuse_tail): a coarse piece is held until the next piece is planned; if that
+    // is its bucket's tail split, both go out as one launch.
+    mh::Piece held;
+    bool have_held = false;
+    auto fusable = [&](const mh::Piece& t) {
+        if (!(t.tail && t.kind == 0 && t.J == held.J && t.mode == held.mode && t.digits == held.digits &&
+              held.first + held.count == t.first && c->noff < kNextSlots && c->qoff < kQueueSlots))
+            return false;
+        bool ok = false;
+        return mh::fast_queue_ok(c->dev, held.J, held.mode, &ok) == hipSuccess && ok;
+    };
     mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
+        if (have_held) {
+            have_held = false;
+            if (fusable(p)) {
+                err = enqueue_piece(c, held, opt, split, &p);
+                return err == MH_OK;
+            }
+            err = enqueue_piece(c, held, opt, split);
+            if (err) return false;
+        }
+        if (opt.fuse_tail && opt.queue && p.kind == 0 && p.L == opt.lower_digits) {
+            held = p;
+            have_held = true;
+            return true;
+        }
         err = enqueue_piece(c, p, opt, split);
         return err == MH_OK;
     });
+    if (!err && have_held) err = enqueue_piece(c, held, opt, split);
     if (!err) err = flush_partials(c, split);
     if (err) {
         for (auto ps : c->ps)

@@ -420,7 +420,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             }
         }
         auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, int Lx, int Jx, int modex, int nbx,
-                             const FastArgs& fax, int finest = 0) -> bool {  // runs [ua, ub) of 10^Lx nonces
+                             const FastArgs& fax, int finest = 0, int tail = 0) -> bool {  // runs [ua, ub) of 10^Lx nonces
             const unsigned __int128 Rx = kPow10[Lx];
             const uint64_t max_runs =
                 std::max<uint64_t>(1u, std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx));
@@ -439,6 +439,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
                 p.blocks = nbx;
                 p.fa = fax;
                 p.finest = finest;
+                p.tail = tail;
                 { const NonceCost nc = nonce_cost(Jx, modex); p.ops = nc.ops; p.slots = nc.slots; }
                 p.fa.u_start = (uint64_t)u;
                 p.fa.n_runs = (uint32_t)runs;
@@ -449,7 +450,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             return true;
         };
         if (!emit_runs(U0, U_split, L, J, mode, nb, fa)) return;
-        if (U_split < U1p && !emit_runs(U_split * 10u, U_fin, Lf, Jf, modef, nbf, faf)) return;
+        if (U_split < U1p && !emit_runs(U_split * 10u, U_fin, Lf, Jf, modef, nbf, faf, 0, 1)) return;
         if (U_fin < U1p * 10u && !emit_runs(U_fin * 10u, U1p * 100u, Lff, Jff, modeff, nbff, faff, 1)) return;
         if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
     }

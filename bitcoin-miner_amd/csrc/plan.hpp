@@ -44,6 +44,7 @@ struct Piece {
     uint32_t ops;     // fast only: nonce_cost(J, mode).ops
     uint32_t slots;   // fast only: nonce_cost(J, mode).slots
     int finest;       // fast only: 1 for the finest tail of a bucket (PlanOpts.finest_tail)
+    int tail;         // fast only: 1 for the tail split of a bucket (PlanOpts.fine_tail)
     FastArgs fa;      // kind 0
     GenArgs ga;       // both (generic launch args; also used by hash_batch)
 };
@@ -96,6 +97,10 @@ struct PlanOpts {
     // more at L - 2, marked `finest` and run on the lowest-priority stream, the other non-coarse
     // pieces then on a normal-priority one, so the search ends on 10-nonce lanes.
     uint64_t finest_tail = 0;
+    // Execution (experiment, 0: off): each bucket's tail split rides in the launch of the coarse
+    // piece before it, as the last chunks of the same work queue (FastArgs.next), instead of a
+    // launch of its own on the low-priority stream.
+    int fuse_tail = 0;
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

@@ -317,7 +317,7 @@ def test_embedded_code_object_carries_queue_marker():
     md = codeobj.metadata(co)
     fast = [k for k in md["amdhsa.kernels"] if "fast_search" in k[".name"]]
     assert len(fast) == 22
-    assert {k[".args"][0][".size"] for k in fast} == {472}      # FastArgs, by value
+    assert {k[".args"][0][".size"] for k in fast} == {488}      # FastArgs, by value
     nomarker = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
     if os.path.exists(nomarker):
         assert b"mh_fast_queue_args" not in open(nomarker, "rb").read()

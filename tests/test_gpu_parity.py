@@ -181,6 +181,17 @@ def test_plan_invariance_small(gpu):
             with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
                      MINEHIP_STREAMS=2, MINEHIP_FINE_TAIL=200_000, MINEHIP_FINEST_TAIL=ft):
                 assert gpu.search(m, lo, hi) == exp, (m[:8], ft)
+        # the tail split fused into the coarse launch before it (MINEHIP_FUSE_TAIL), also with tiny
+        # grids (many launches, partial-buffer flushes) and without the work queue (no fusion)
+        for fu in (0, 1):
+            for st, ft, mb, q in ((1, 20_000, 0, 1), (2, 20_000, 0, 1), (2, 200_000, 0, 1), (2, 200_000, 3, 1),
+                                  (2, 200_000, 0, 0)):
+                kv = dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
+                          MINEHIP_QUEUE=q, MINEHIP_FUSE_TAIL=fu)
+                if mb:
+                    kv["MINEHIP_MAX_BLOCKS"] = mb
+                with env(**kv):
+                    assert gpu.search(m, lo, hi) == exp, (m[:8], fu, st, ft, mb, q)
         # which full-L pieces take the high-priority stream (MINEHIP_COARSE_MIN)
         for cm in (1, 100_000, 1 << 62):
             with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
@@ -203,6 +214,9 @@ def test_full_size_properties(gpu, msg, bits):
     hi = (1 << bits) - 1
     r = gpu.search(msg, 0, hi)
     assert oracle.hash_(msg, r[1]) == r[0] and 0 <= r[1] <= hi  # re-hashes to itself
+    for fu in (0, 1):  # tail splits in launches of their own / fused into the coarse launches
+        with env(MINEHIP_FUSE_TAIL=fu):
+            assert gpu.search(msg, 0, hi) == r, fu
     rng = random.Random(bits)
     for _ in range(2):  # split-range associativity
         mid = rng.randrange(1, hi)
