@@ -333,7 +333,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 // on them -- tests/test_gpu_parity.py checks exactly that):
 //   MINEHIP_LOWER_DIGITS   L, digits enumerated inside one lane (1..5, default 3)
 //   MINEHIP_MIN_LANES      lower L per bucket until it has this many runs (2^19)
-//   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^34)
+//   MINEHIP_LAUNCH_NONCES  nonces per fast launch (default 2^35)
 //   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
 //   MINEHIP_MAX_BLOCKS     workgroups per launch (1..kMaxBlocksPerLaunch)
 //   MINEHIP_STREAMS        1: one stream; 2: coarse / fine pieces on high / low priority
