@@ -32,3 +32,37 @@ def test_design_states_the_shipped_defaults():
     assert set(code) == set(doc), (sorted(code), sorted(doc))
     for k, v in code.items():
         assert doc[k] == v, (k, doc[k], v)
+
+
+def _num(v):
+    v = v.strip().strip("`")
+    m = re.fullmatch(r"2\^(\d+)", v)
+    return 2 ** int(m.group(1)) if m else int(v)
+
+
+def plan_opts_env():
+    src = open(os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "minehip.cpp")).read()
+    body = src[src.index("mh::PlanOpts plan_opts()"):]
+    body = body[:body.index("\n}\n")]
+    return set(re.findall(r'getenv\("(MINEHIP_\w+)"\)', body))
+
+
+def integration_knobs():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc[doc.index("| Variable | Default | Meaning |"):]
+    sec = sec[:sec.index("\n\n")]
+    return {k: v for k, v in re.findall(r"^\| `(MINEHIP_\w+)` \| ([^|]+) \|", sec, flags=re.M)}
+
+
+def test_integration_knobs_match_the_library():
+    """INTEGRATION.md's table of planner knobs names exactly the variables plan_opts() reads, with
+    PlanOpts' defaults (the field each one sets is DESIGN.md §3's table)."""
+    knobs = integration_knobs()
+    assert set(knobs) == plan_opts_env(), (sorted(knobs), sorted(plan_opts_env()))
+    doc = open(os.path.join(ROOT, "DESIGN.md")).read()
+    sec = doc[doc.index("**Shipped defaults**"):doc.index("**Two streams.**")]
+    field_of = {env: f for f, env in re.findall(r"^\| `(\w+)`[^|]*\|[^|]*\| `(MINEHIP_\w+)`", sec, flags=re.M)}
+    code = plan_defaults()
+    for env, default in knobs.items():
+        assert env in field_of, env
+        assert _num(default) == _num(code[field_of[env]]), (env, default, code[field_of[env]])
