@@ -505,7 +505,7 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
         return None
     lib = ctypes.CDLL(path)
     lib.cp_start.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
-    lib.cp_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    lib.cp_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     lo, n = 10 ** 11, 1 << 37  # d = 12: last digit in word 4, the configs[1] d = 10 bucket's layout
     if lib.cp_start(dev, delay_s, window_s, nwg) != 0:
         return None
@@ -515,7 +515,7 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
         search_dev("cmu440", lo, lo + n - 1)
         search_s = time.perf_counter() - t
     finally:
-        rc = lib.cp_read(buf, nwg)  # always: waits for the probes and frees their buffer
+        rc = lib.cp_read(dev, buf, nwg)  # always: waits for the probes and frees their buffer
     if rc != 0:
         return None
     rows = [tuple(buf[4 * i:4 * i + 4]) for i in range(nwg)]
@@ -540,6 +540,29 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
                     "fast_search<4, One> (tools/clock_probe.hip)"}
 
 
+def kernel_clocks(search_on, devices, probe=None):
+    """kernel_clock on every device at once, one host thread per device (the in-process N-GPU
+    path): each device runs its own 2^37-nonce search with its probe inside,
+    so the clocks are those of N devices under load together, as in the timed region.
+    search_on(dev) -> search_dev for that device.  Returns {dev: kernel_clock result or None}."""
+    import threading
+    probe = probe or kernel_clock
+    out = {}
+
+    def run(d):
+        try:
+            out[d] = probe(search_on(d), d)
+        except Exception as e:  # a failed probe leaves that device's clock unknown, not the line
+            out[d] = {"ghz": None, "note": f"probe failed: {e}"}
+
+    th = [threading.Thread(target=run, args=(d,)) for d in sorted(set(devices))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    return out
+
+
 def rank_device(local, ndev):
     """The HIP device of a launched rank: LOCAL_RANK when the process sees every GPU of the node,
     device 0 when the launcher gives each rank exactly one visible GPU (HIP/ROCR_VISIBLE_DEVICES
@@ -559,16 +582,33 @@ def ranks_per_device(idents):
     return max(Counter(tuple(i) for i in idents).values()) if idents else 0
 
 
-def same_workload_n1(search_dev, steps):
-    """One step of the scaling workload on ONE device: BASELINE configs[3]'s middle slice
-    ("cmu440", 2^40 / K nonces with K = max(steps, 20): the driver's --steps 20 step) searched
-    alone.  The N > 1 lines run configs[3] and the N = 1 line configs[1], so the driver's 1 -> N
-    ratio would otherwise compare two workloads; every line carries this N = 1 figure of the same
-    work (`n1_config4_ghs`) and, for configs[3] lines, value / (N x it) (`per_gpu_efficiency`)."""
-    cfg = CONFIGS["4"]
+N1_CHUNK_BITS = 32  # tests/golden/fullsize_cfg4.json: the minimum of every 2^32 chunk of configs[3]
+
+
+def n1_slice(steps):
+    """The configs[3] slice same_workload_n1 searches: the whole 2^32 chunks nearest to one step of
+    K = max(steps, 20) (the driver's --steps 20 step: 12.8 chunks -> 13), from the chunk boundary
+    at or below the middle step's start, so that tests/golden/fullsize_cfg4.json's chunk minima
+    pin its result bit for bit."""
     k_all = max(steps, 20)
     k = k_all // 2
-    lo, hi = step_range(cfg, k, k_all)
+    s_lo, s_hi = step_range(CONFIGS["4"], k, k_all)
+    c = 1 << N1_CHUNK_BITS
+    n = max(1, round((s_hi - s_lo + 1) / c))
+    lo = s_lo // c * c
+    return lo, lo + n * c - 1, f"step {k} of {k_all}, rounded to {n} whole 2^{N1_CHUNK_BITS} chunks"
+
+
+def same_workload_n1(search_dev, steps):
+    """One step of the scaling workload on ONE device: BASELINE configs[3]'s middle slice
+    ("cmu440", ~2^40 / K nonces with K = max(steps, 20): the driver's --steps 20 step, rounded to
+    whole fixture chunks, n1_slice) searched alone.  The N > 1 lines run configs[3] and the N = 1
+    line configs[1], so the driver's 1 -> N ratio would otherwise compare two workloads; every line
+    carries this N = 1 figure of the same work (`n1_config4_ghs`) and, for configs[3] lines,
+    value / (N x it) (`per_gpu_efficiency`).  Its result is checked against the fixture
+    (`golden_ok`)."""
+    cfg = CONFIGS["4"]
+    lo, hi, what = n1_slice(steps)
     msg = cfg["msg"].encode()
     search_dev(msg, lo, lo + (1 << 30) - 1)  # untimed: device context, module and clocks up
     t = time.perf_counter()
@@ -576,7 +616,7 @@ def same_workload_n1(search_dev, steps):
     dt = time.perf_counter() - t
     expect = golden_expect(msg, lo, hi)
     return {"ghs": round((hi - lo + 1) / dt / 1e9, 4), "ms": round(dt * 1e3, 3), "range": [lo, hi],
-            "slice": f"step {k} of {k_all}", "result": list(r),
+            "slice": what, "result": list(r),
             "golden_ok": None if expect is None else tuple(r) == expect}
 
 
@@ -870,6 +910,12 @@ def main():
         kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
         for p in per_dev:
             p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
+    elif multi and not args.no_clock:
+        # the in-process path: every device's clock at once, one host thread per device
+        kcs = kernel_clocks(lambda d: (lambda m, a, b: minehip.search(m, a, b, d)), uniq)
+        for p in per_dev:
+            kc = kcs.get(p["dev"])
+            p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
 
     t_max = elapsed
     if launched:
@@ -990,6 +1036,7 @@ def main():
         if multi:  # the rates the library sized the last step's shards by (cost units per ns)
             for pd, rate in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
                 pd["multi_rate"] = round(rate, 1)
+        clocks = [p["kernel_clock_ghz"] for p in per_device if p.get("kernel_clock_ghz")]
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -1010,6 +1057,10 @@ def main():
             # the scaling workload on one device (same_workload_n1): the N = 1 point of a configs[3]
             # curve, and this line's value against N times it when the line runs configs[3]
             "n1_config4_ghs": n1["ghs"] if n1 else None,
+            # N > 1: the slowest and fastest device's in-kernel clock during a concurrent search after
+            # the timed region -- with per_gpu_efficiency, whether a shortfall is clock spread between
+            # power-limited devices or scheduling
+            "kernel_clock_ghz_range": [min(clocks), max(clocks)] if n_gpus > 1 and clocks else None,
             "per_gpu_efficiency": (per_gpu_efficiency(value, n_gpus, n1["ghs"])
                                    if n1 and cfg_name == "4" and args.bits is None and args.msg is None else None),
             "n1_config4": n1,
@@ -1029,6 +1080,8 @@ def main():
                            "one process, mh_search_multi: one host thread + HIP stream per device" if multi else
                            "one process, mh_search on one device"),
                 "parallelism": f"contiguous shards over {n_gpus} GPU(s), 16-byte (hash, nonce) host merge, no RCCL",
+                # in-process: the device of every worker (a repeat rehearses N workers on fewer GPUs)
+                "devices": devs if multi else None,
                 # launched: the most ranks one physical GPU served (1 = one GPU per rank)
                 "ranks_per_device": shared if launched else None,
                 "shards": ("each strong step split in proportion to every rank's measured search rate "

@@ -353,30 +353,20 @@ __global__ __launch_bounds__(kBlockThreads, min_waves(J, MODE)) void fast_search
     // The chunk body reads its arguments through a pointer the loop launders every iteration,
     // so the compiler cannot keep values derived from them live from one chunk to the next:
     // hoisted out of the loop they spilled ~240 SGPRs into VGPR lanes (85 VGPRs instead of 70).
-    // Fused tail (a.next): the chunks past a.n_chunks run the args at a.next (the bucket's last
-    // runs at L - 1, read like the kernel arguments through a scalar pointer), partials after a's.
     using KArgs = __attribute__((address_space(4))) const FastArgs;
-    KArgs* kp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-    const uint32_t n_all = a.n_chunks + (a.next ? a.next_chunks : 0u);
+    KArgs* const kp = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     uint32_t blk = a.counter ? claim_chunk(a.counter) : blockIdx.x;
-    while (blk < n_all) {
+    while (blk < a.n_chunks) {
         KArgs* k = kp;
-        Partial* out = partials;
-        uint32_t b = blk;
-        if (blk >= a.n_chunks) {
-            k = (KArgs*)(uintptr_t)a.next;
-            out = partials + a.n_chunks;
-            b = blk - a.n_chunks;
-        }
         asm volatile("" : "+s"(k));
-        fast_chunk<J, MODE>(*(const FastArgs*)k, out, b);
+        fast_chunk<J, MODE>(*(const FastArgs*)k, partials, blk);
         if (!a.counter) break;
         blk = claim_chunk(a.counter);
     }
 }
 
-// Marker of a code object whose fast_search kernels run the work-queue loop above (with the fused
-// tail) over this FastArgs layout: its size is sizeof(FastArgs).  The library uses the work queue with a code
+// Marker of a code object whose fast_search kernels run the work-queue loop above over this
+// FastArgs layout: its size is sizeof(FastArgs).  The library uses the work queue with a code
 // object only if it carries the marker at that size (search_kernels.hip, fast_function) -- the
 // embedded object always does; one loaded by the dev build's MINEHIP_DEV_CODE_OBJECT hook from
 // older sources runs one workgroup per chunk instead of searching only its first chunks.

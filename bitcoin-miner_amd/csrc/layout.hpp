@@ -49,13 +49,6 @@ struct FastArgs {
     // counter until it passes n_chunks, so an XCD that clocks faster takes more of them;
     // null -> workgroup b runs chunk b (grid = n_chunks).  DESIGN.md §3.
     uint32_t* counter;
-    // Fused tail (work queue only, null: none): chunk indices [n_chunks, n_chunks + next_chunks)
-    // run the args at `next` (device memory) -- the same bucket's last runs at L - 1, so the
-    // launch ends on 100-nonce lanes and drains ~10x sooner -- writing their partials after this
-    // launch's own.  DESIGN.md §3.
-    const FastArgs* next;
-    uint32_t next_chunks;
-    uint32_t pad_;
 };
 
 // Arguments of the generic per-nonce kernels (range edges, small buckets,

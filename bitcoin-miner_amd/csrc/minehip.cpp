@@ -30,7 +30,6 @@
 namespace mh {
 hipError_t fast_module_init(int dev);
 hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, hipStream_t s);
-hipError_t fast_queue_ok(int dev, int J, int mode, bool* ok);
 hipError_t launch_generic_scan(const GenArgs& a, Partial* partials, uint32_t blocks, hipStream_t s);
 hipError_t launch_hash_batch(const GenArgs& a, const uint64_t* d_nonces, uint64_t* d_out, uint64_t n,
                              hipStream_t s);
@@ -65,7 +64,6 @@ namespace {
 constexpr uint64_t kBatchChunk = 1u << 22;  // nonces per hash_batch transfer
 constexpr int kEventPairs = 512;             // profiled launches buffered before harvesting
 constexpr uint32_t kQueueSlots = 4096;       // work-queue counters per search (one per fast launch)
-constexpr uint32_t kNextSlots = 256;         // fused-tail argument blocks per search (one per fused launch)
 
 struct Timed {
     hipEvent_t start = nullptr, stop = nullptr;
@@ -85,10 +83,9 @@ struct DevCtx {
     int dev = -1;
     bool ready = false;
     hipStream_t stream = nullptr;              // every search's merge and copy; pieces with streams = 1
-    // streams = 2: the pieces' streams, by priority: [0] coarse pieces (highest), [1] the other pieces
-    // when a finest tail is planned (normal), [2] the other pieces, or the finest tail (lowest)
-    hipStream_t ps[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_piece[3] = {nullptr, nullptr, nullptr};  // each piece stream's work so far
+    // streams = 2: the pieces' streams, by priority: [0] coarse pieces (high), [1] the other pieces (low)
+    hipStream_t ps[2] = {nullptr, nullptr};
+    hipEvent_t ev_piece[2] = {nullptr, nullptr};  // each piece stream's work so far
     hipEvent_t ev_main = nullptr;                          // the main stream's (reset / merge)
     Partial* d_partials = nullptr;
     Partial* d_best = nullptr;
@@ -98,9 +95,6 @@ struct DevCtx {
     uint32_t poff = 0;  // partials written since the last merge
     uint32_t* d_counters = nullptr;  // work-queue counters, zeroed at each search's start
     uint32_t qoff = 0;               // counters used by this search
-    mh::FastArgs* d_next = nullptr;  // fused tails' arguments (device), staged through
-    mh::FastArgs* h_next = nullptr;  // ... pinned host slots; one per fused launch of a search
-    uint32_t noff = 0;               // slots used by this search
     // profiling
     bool prof = false;
     std::vector<Timed> pool;
@@ -145,11 +139,11 @@ int init_locked(DevCtx* c, int dev) {
     // each resource only once: a call after a failed init (e.g. the code object
     // did not load) resumes where that one stopped instead of allocating again
     if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (!c->ps[0] || !c->ps[2]) {  // ps[1] only once a search plans a finest tail (ensure_mid_stream)
+    if (!c->ps[0] || !c->ps[1]) {
         int least = 0, greatest = 0;
         MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));  // gfx950: 1 .. -1
         if (!c->ps[0]) MH_HIP(hipStreamCreateWithPriority(&c->ps[0], hipStreamNonBlocking, greatest));
-        if (!c->ps[2]) MH_HIP(hipStreamCreateWithPriority(&c->ps[2], hipStreamNonBlocking, least));
+        if (!c->ps[1]) MH_HIP(hipStreamCreateWithPriority(&c->ps[1], hipStreamNonBlocking, least));
     }
     for (auto& e : c->ev_piece)
         if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -158,8 +152,6 @@ int init_locked(DevCtx* c, int dev) {
     if (!c->d_best) MH_HIP(hipMalloc(&c->d_best, sizeof(Partial)));
     if (!c->d_counters) MH_HIP(hipMalloc(&c->d_counters, sizeof(uint32_t) * kQueueSlots));
     if (!c->h_best) MH_HIP(hipHostMalloc(&c->h_best, sizeof(Partial), hipHostMallocDefault));
-    if (!c->d_next) MH_HIP(hipMalloc(&c->d_next, sizeof(mh::FastArgs) * kNextSlots));
-    if (!c->h_next) MH_HIP(hipHostMalloc(&c->h_next, sizeof(mh::FastArgs) * kNextSlots, hipHostMallocDefault));
     if (!c->d_nonces) MH_HIP(hipMalloc(&c->d_nonces, sizeof(uint64_t) * kBatchChunk));
     if (!c->d_hashes) MH_HIP(hipMalloc(&c->d_hashes, sizeof(uint64_t) * kBatchChunk));
     if (c->pool.empty()) c->pool.resize(kEventPairs);
@@ -186,31 +178,20 @@ int harvest_locked(DevCtx* c) {
     return MH_OK;
 }
 
-// Fold the pending partials into the running minimum.  With two piece
-// streams the merge (on the main stream) first waits for both, and both wait
-// for the merge before any later piece reuses the partials buffer.
-// The normal-priority piece stream, created when a search first plans a finest tail.
-int ensure_mid_stream(DevCtx* c) {
-    if (c->ps[1]) return MH_OK;
-    int least = 0, greatest = 0;
-    MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    MH_HIP(hipStreamCreateWithPriority(&c->ps[1], hipStreamNonBlocking, (least + greatest) / 2));
-    return MH_OK;
-}
-
 // The piece streams start after the main stream's work so far (the reset, a merge).
 int piece_streams_wait_main(DevCtx* c) {
     MH_HIP(hipEventRecord(c->ev_main, c->stream));
-    for (auto s : c->ps)
-        if (s) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
+    for (auto s : c->ps) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
     return MH_OK;
 }
 
+// Fold the pending partials into the running minimum.  With two piece
+// streams the merge (on the main stream) first waits for both, and both wait
+// for the merge before any later piece reuses the partials buffer.
 int flush_partials(DevCtx* c, bool split) {
     if (!c->poff) return MH_OK;
     if (split) {
-        for (int k = 0; k < 3; ++k) {
-            if (!c->ps[k]) continue;
+        for (int k = 0; k < 2; ++k) {
             MH_HIP(hipEventRecord(c->ev_piece[k], c->ps[k]));
             MH_HIP(hipStreamWaitEvent(c->stream, c->ev_piece[k], 0));
         }
@@ -221,28 +202,15 @@ int flush_partials(DevCtx* c, bool split) {
     return MH_OK;
 }
 
+// Coarse pieces (the full L: 1,000-nonce lanes) go to the high-priority stream, the others
+// (shorter lanes, generic edges, the tail split) to the low-priority one.
+bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) { return p.kind == 0 && p.L == opt.lower_digits; }
+
 // Enqueue one piece on the context's stream.  Its workgroups write their
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
-bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) {
-    return p.kind == 0 && p.L == opt.lower_digits && p.count >= opt.coarse_min;
-}
-
-// The piece stream of p (streams = 2): coarse pieces on the highest priority; the finest tail, when
-// planned, on the lowest, below every other piece (normal priority then), so that it is dispatched
-// last and its short workgroups fill the drain of the search's last pieces.
-hipStream_t piece_stream(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt) {
-    if (coarse_piece(p, opt)) return c->ps[0];
-    if (p.finest) return c->ps[2];
-    return opt.finest_tail ? c->ps[1] : c->ps[2];
-}
-
-// tail (optional): the bucket's tail split, fused into p's launch (PlanOpts.fuse_tail; the caller
-// checked fusable()).
-int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split,
-                  const mh::Piece* tail = nullptr) {
-    // split: coarse pieces (the full L) on the high-priority stream, the rest on the low one
-    hipStream_t s = !split ? c->stream : piece_stream(c, p, opt);
+int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
+    hipStream_t s = !split ? c->stream : c->ps[coarse_piece(p, opt) ? 0 : 1];
     uint32_t blocks;
     if (p.kind == 0) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
@@ -255,15 +223,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
             return fail(MH_EINTERNAL, "internal: bad generic piece");
         blocks = (uint32_t)((p.ga.count + mh::kBlockThreads - 1) / mh::kBlockThreads);
     }
-    uint32_t tail_blocks = 0;
-    if (tail) {
-        if (tail->kind != 0 || tail->fa.n_runs == 0 || tail->fa.L < 1 || tail->fa.n_hi + tail->fa.L > 20 ||
-            tail->J != p.J || tail->mode != p.mode)
-            return fail(MH_EINTERNAL, "internal: bad fused tail");
-        tail_blocks = (tail->fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
-    }
-    if (blocks + tail_blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
-    if (c->poff + blocks + tail_blocks > mh::kMaxBlocksPerLaunch) {
+    if (blocks > mh::kMaxBlocksPerLaunch) return fail(MH_EINTERNAL, "internal: grid too large");
+    if (c->poff + blocks > mh::kMaxBlocksPerLaunch) {
         const int rc = flush_partials(c, split);
         if (rc) return rc;
     }
@@ -274,27 +235,11 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
         fa.n_chunks = blocks;
         // work queue while this search has counters left (a longer search runs the rest static)
         fa.counter = (opt.queue && c->qoff < kQueueSlots) ? c->d_counters + c->qoff++ : nullptr;
-        fa.next = nullptr;
-        fa.next_chunks = 0;
-        if (tail) {
-            if (!fa.counter || c->noff >= kNextSlots) return fail(MH_EINTERNAL, "internal: no slot for a fused tail");
-            mh::FastArgs* h = c->h_next + c->noff;
-            *h = tail->fa;
-            h->n_chunks = tail_blocks;
-            h->counter = nullptr;
-            h->next = nullptr;
-            h->next_chunks = 0;
-            fa.next = c->d_next + c->noff++;
-            fa.next_chunks = tail_blocks;
-            // stream-ordered before the launch; the slot is not rewritten before the search's end sync
-            MH_HIP(hipMemcpyAsync((void*)fa.next, h, sizeof(mh::FastArgs), hipMemcpyHostToDevice, s));
-        }
     }
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
-            for (auto ps : c->ps)
-                if (ps) MH_HIP(hipStreamSynchronize(ps));
+            for (auto ps : c->ps) MH_HIP(hipStreamSynchronize(ps));
             int rc = harvest_locked(c);
             if (rc) return rc;
         }
@@ -308,11 +253,10 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     else
         MH_HIP(mh::launch_generic_scan(p.ga, out, blocks, s));
     if (tm) MH_HIP(hipEventRecord(tm->stop, s));
-    c->poff += blocks + tail_blocks;
+    c->poff += blocks;
     if (c->prof) {
         if (p.kind == 0) {
-            // a fused tail's nonces count with the launch they ran in (same kernel, same nonce_ops)
-            const uint64_t n = p.count + (tail ? tail->count : 0u);
+            const uint64_t n = p.count;
             c->cnt[0] += 1;
             c->cnt[1] += n;
             c->cnt[3] += n * (uint64_t)p.ops;
@@ -342,11 +286,6 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //                          2^28; 0: none)
 //   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
 //                          XCDs take more; default); 0: one workgroup per chunk
-//   MINEHIP_COARSE_MIN     full-L pieces smaller than this go to the low-priority stream (0)
-//   MINEHIP_FINEST_TAIL    nonces at the end of each tail split planned at L - 2, on the lowest-
-//                          priority stream (0: none)
-//   MINEHIP_FUSE_TAIL      1: each tail split runs as the last chunks of the coarse launch before
-//                          it (work queue only); 0: a launch of its own (default)
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -371,12 +310,6 @@ mh::PlanOpts plan_opts() {
     if (const char* e = getenv("MINEHIP_QUEUE")) {
         const int v = atoi(e);
         if (v == 0 || v == 1) o.queue = v;
-    }
-    if (const char* e = getenv("MINEHIP_COARSE_MIN")) o.coarse_min = strtoull(e, nullptr, 10);
-    if (const char* e = getenv("MINEHIP_FINEST_TAIL")) o.finest_tail = strtoull(e, nullptr, 10);
-    if (const char* e = getenv("MINEHIP_FUSE_TAIL")) {
-        const int v = atoi(e);
-        if (v == 0 || v == 1) o.fuse_tail = v;
     }
     return o;
 }
@@ -415,46 +348,15 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
         });
     const bool split = opt.streams == 2 && any_coarse && any_fine;
     if (split) {  // the piece streams start after the reset (and after the previous search)
-        if (opt.finest_tail) {
-            rc = ensure_mid_stream(c);
-            if (rc) return rc;
-        }
         rc = piece_streams_wait_main(c);
         if (rc) return rc;
     }
     int err = MH_OK;
     c->poff = 0;
-    c->noff = 0;
-    // Fused tails (opt.fuse_tail): a coarse piece is held until the next piece is planned; if that
-    // is its bucket's tail split, both go out as one launch.
-    mh::Piece held;
-    bool have_held = false;
-    auto fusable = [&](const mh::Piece& t) {
-        if (!(t.tail && t.kind == 0 && t.J == held.J && t.mode == held.mode && t.digits == held.digits &&
-              held.first + held.count == t.first && c->noff < kNextSlots && c->qoff < kQueueSlots))
-            return false;
-        bool ok = false;
-        return mh::fast_queue_ok(c->dev, held.J, held.mode, &ok) == hipSuccess && ok;
-    };
     mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
-        if (have_held) {
-            have_held = false;
-            if (fusable(p)) {
-                err = enqueue_piece(c, held, opt, split, &p);
-                return err == MH_OK;
-            }
-            err = enqueue_piece(c, held, opt, split);
-            if (err) return false;
-        }
-        if (opt.fuse_tail && opt.queue && p.kind == 0 && p.L == opt.lower_digits) {
-            held = p;
-            have_held = true;
-            return true;
-        }
         err = enqueue_piece(c, p, opt, split);
         return err == MH_OK;
     });
-    if (!err && have_held) err = enqueue_piece(c, held, opt, split);
     if (!err) err = flush_partials(c, split);
     if (err) {
         for (auto ps : c->ps)
@@ -556,50 +458,64 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     std::string err_msg;
     auto now = []() { return now_ns(); };
     std::vector<std::thread> th;
-    for (int i = 0; i < ndev; ++i) {
-        th.emplace_back([&, i]() {
-            for (;;) {
-                uint64_t seen;
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    if (done) return;
-                    seen = gen;
-                }
-                mh_assignment a;
-                if (sched.next(i, now(), &a) != 1) {
-                    // nothing to hand out: wait for the job to finish, or for a
-                    // failed device's chunk to come back
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return done || gen != seen; });
-                    continue;
-                }
-                uint64_t h, nn;
-                const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
-                                                 : search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
-                if (r) {
-                    const std::string e = g_err;
-                    sched.remove_miner(i);  // its chunk goes back to the job
-                    std::lock_guard<std::mutex> lk(mu);
-                    if (!first_err) {
-                        first_err = r;
-                        err_msg = e;
-                    }
-                    if (--alive == 0) done = true;
-                    ++gen;
-                    cv.notify_all();
-                    return;
-                }
-                mh_completion c;
-                const int q = sched.result(i, h, nn, now(), &c);
+    auto miner = [&](int i) {
+        for (;;) {
+            uint64_t seen;
+            {
                 std::lock_guard<std::mutex> lk(mu);
-                if (q == 1) {
-                    res = c;
-                    done = true;
+                if (done) return;
+                seen = gen;
+            }
+            mh_assignment a;
+            if (sched.next(i, now(), &a) != 1) {
+                // nothing to hand out: wait for the job to finish, or for a
+                // failed device's chunk to come back
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return done || gen != seen; });
+                continue;
+            }
+            uint64_t h, nn;
+            const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
+                                             : search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
+            if (r) {
+                const std::string e = g_err;
+                sched.remove_miner(i);  // its chunk goes back to the job
+                std::lock_guard<std::mutex> lk(mu);
+                if (!first_err) {
+                    first_err = r;
+                    err_msg = e;
                 }
+                if (--alive == 0) done = true;
                 ++gen;
                 cv.notify_all();
+                return;
             }
-        });
+            mh_completion c;
+            const int q = sched.result(i, h, nn, now(), &c);
+            std::lock_guard<std::mutex> lk(mu);
+            if (q == 1) {
+                res = c;
+                done = true;
+            }
+            ++gen;
+            cv.notify_all();
+        }
+    };
+    try {
+        for (int i = 0; i < ndev; ++i) th.emplace_back(miner, i);
+    } catch (...) {
+        // out of threads: the miners that did not start leave the scheduler (their chunks, if
+        // any, go back to the job) and the started ones finish the job
+        for (size_t i = th.size(); i < (size_t)ndev; ++i) sched.remove_miner((int64_t)i);
+        std::lock_guard<std::mutex> lk(mu);
+        alive -= ndev - (int)th.size();
+        if (!first_err) {
+            first_err = MH_EINTERNAL;
+            err_msg = "could not start a host thread per device";
+        }
+        if (alive == 0) done = true;
+        ++gen;
+        cv.notify_all();
     }
     for (auto& t : th) t.join();
     if (alive == 0) return fail(first_err ? first_err : MH_EHIP, err_msg.empty() ? "every device failed" : err_msg);
@@ -772,7 +688,7 @@ int64_t mh_multi_plan(const uint8_t* msg, size_t len, uint64_t lower, uint64_t u
 
 int mh_multi_rates(const int* devs, int ndev, double* out) {
     g_err.clear();
-    if (!devs || !out || ndev < 0) return fail(MH_EINVAL, "bad arguments");
+    if (ndev < 0 || (ndev > 0 && (!devs || !out))) return fail(MH_EINVAL, "bad arguments");
     for (int i = 0; i < ndev; ++i) out[i] = mh::device_rate(devs[i]);
     return MH_OK;
 }

@@ -46,6 +46,14 @@ std::vector<double> worker_weights(const int* devs, int ndev) {
     const double fill = known ? sum / known : 1.0;
     for (auto& x : w)
         if (x <= 0.0) x = fill;
+    // A device listed k times runs its k shards one after another (one search at a time per
+    // device), so each entry gets 1/k of its device's rate: every physical device then carries a
+    // share of the range in proportion to its own rate.
+    for (int i = 0; i < ndev; ++i) {
+        int k = 0;
+        for (int j = 0; j < ndev; ++j) k += devs[j] == devs[i];
+        w[(size_t)i] /= (double)k;
+    }
     return w;
 }
 

@@ -407,20 +407,8 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
                 Lf = L - 1;
             }
         }
-        // Finest tail (opt.finest_tail): the last runs of the tail split once more at L - 2.
-        unsigned __int128 U_fin = U1p * 10u;  // tail runs (10^Lf nonces) [U_split*10, U_fin), then finest
-        int Lff = 0, Jff = 0, modeff = 0, nbff = 1;
-        FastArgs faff;
-        if (Lf >= 2 && opt.finest_tail) {
-            const unsigned __int128 fin_runs = opt.finest_tail / (uint64_t)kPow10[Lf];
-            if (fin_runs >= 1 && (U1p - U_split) * 10u > 4 * fin_runs &&
-                make_fast_args(pre, d, Lf - 1, &Jff, &modeff, &nbff, &faff)) {
-                U_fin = U1p * 10u - fin_runs;
-                Lff = Lf - 1;
-            }
-        }
         auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, int Lx, int Jx, int modex, int nbx,
-                             const FastArgs& fax, int finest = 0, int tail = 0) -> bool {  // runs [ua, ub) of 10^Lx nonces
+                             const FastArgs& fax) -> bool {  // runs [ua, ub) of 10^Lx nonces
             const unsigned __int128 Rx = kPow10[Lx];
             const uint64_t max_runs =
                 std::max<uint64_t>(1u, std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx));
@@ -438,8 +426,6 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
                 p.mode = modex;
                 p.blocks = nbx;
                 p.fa = fax;
-                p.finest = finest;
-                p.tail = tail;
                 { const NonceCost nc = nonce_cost(Jx, modex); p.ops = nc.ops; p.slots = nc.slots; }
                 p.fa.u_start = (uint64_t)u;
                 p.fa.n_runs = (uint32_t)runs;
@@ -450,8 +436,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             return true;
         };
         if (!emit_runs(U0, U_split, L, J, mode, nb, fa)) return;
-        if (U_split < U1p && !emit_runs(U_split * 10u, U_fin, Lf, Jf, modef, nbf, faf, 0, 1)) return;
-        if (U_fin < U1p * 10u && !emit_runs(U_fin * 10u, U1p * 100u, Lff, Jff, modeff, nbff, faff, 1)) return;
+        if (U_split < U1p && !emit_runs(U_split * 10u, U1p * 10u, Lf, Jf, modef, nbf, faf)) return;
         if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
     }
     flush_generic();

@@ -43,8 +43,6 @@ struct Piece {
     int blocks;       // tail blocks of the final message
     uint32_t ops;     // fast only: nonce_cost(J, mode).ops
     uint32_t slots;   // fast only: nonce_cost(J, mode).slots
-    int finest;       // fast only: 1 for the finest tail of a bucket (PlanOpts.finest_tail)
-    int tail;         // fast only: 1 for the tail split of a bucket (PlanOpts.fine_tail)
     FastArgs fa;      // kind 0
     GenArgs ga;       // both (generic launch args; also used by hash_batch)
 };
@@ -90,17 +88,10 @@ struct PlanOpts {
     // with the same code object: +0.6% to +1.9% on configs[1], configs[2]'s halves and the d = 10
     // bucket (profiles/r03u_*).  0: one workgroup per chunk.
     int queue = 1;
-    // Execution: a full-L piece goes to the high-priority stream only if it has at least coarse_min
-    // nonces (smaller ones back-fill from the low-priority stream).  0: every full-L piece.
-    uint64_t coarse_min = 0;
-    // Finest tail (experiment, 0: off): the last finest_tail nonces of each tail split planned once
-    // more at L - 2, marked `finest` and run on the lowest-priority stream, the other non-coarse
-    // pieces then on a normal-priority one, so the search ends on 10-nonce lanes.
-    uint64_t finest_tail = 0;
-    // Execution (experiment, 0: off): each bucket's tail split rides in the launch of the coarse
-    // piece before it, as the last chunks of the same work queue (FastArgs.next), instead of a
-    // launch of its own on the low-priority stream.
-    int fuse_tail = 0;
+    // Round 4 A/B-rejected three more execution knobs and they were removed from the library in
+    // round 5 (HISTORY.md §3): full-L pieces below 2^31 / 2^33 nonces on the low-priority stream
+    // (-4% / -5%), a finest tail at L - 2 on a third stream (+-0.3%), and the tail split fused
+    // into the coarse launch's work queue (-0.2% to -1.0%).
 };
 
 // Calls cb for every piece in increasing nonce order; stops early when cb

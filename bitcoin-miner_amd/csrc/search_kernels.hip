@@ -240,18 +240,9 @@ hipError_t resident_groups(int dev, hipFunction_t f, unsigned lds, uint32_t* out
     return hipSuccess;
 }
 
-// a.n_chunks chunks of 256 runs (+ a.next_chunks of the fused tail at a.next); static (a.counter
-// null): one workgroup per chunk; work queue: as many workgroups as fit at once (an over-estimate
-// only queues some of them), each claiming chunks from a.counter (zeroed by the caller, one
-// counter per launch).
-// The code object's fast_search<J, mode> runs the work-queue loop with the fused tail (its
-// marker is at this library's sizeof(FastArgs)).
-hipError_t fast_queue_ok(int dev, int J, int mode, bool* ok) {
-    if (!fast_variant_exists(J, mode)) return hipErrorInvalidValue;
-    hipFunction_t f;
-    return fast_function(dev, J, mode, &f, ok);
-}
-
+// a.n_chunks chunks of 256 runs; static (a.counter null): one workgroup per chunk; work queue:
+// as many workgroups as fit at once (an over-estimate only queues some of them), each claiming
+// chunks from a.counter (zeroed by the caller, one counter per launch).
 hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* partials, hipStream_t s) {
     if (!fast_variant_exists(J, mode)) return hipErrorInvalidValue;
 #ifdef MH_DEV_HOOKS
@@ -269,13 +260,8 @@ hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* par
     hipError_t e = fast_function(dev, J, mode, &f, &queue_ok);
     if (e != hipSuccess) return e;
     FastArgs args = a;
-    if (!queue_ok) {
-        // a code object without the loop: one workgroup per chunk, and no fused tail
-        if (args.next) return hipErrorInvalidValue;
-        args.counter = nullptr;
-    }
-    if (args.next && !args.counter) return hipErrorInvalidValue;  // the fused tail needs the queue
-    uint32_t grid = args.n_chunks + (args.next ? args.next_chunks : 0u);
+    if (!queue_ok) args.counter = nullptr;  // a code object without the loop: one workgroup per chunk
+    uint32_t grid = args.n_chunks;
     if (args.counter) {
         uint32_t resident = 0;
         e = resident_groups(dev, f, lds, &resident);

@@ -92,6 +92,8 @@ def plan(msg, lower, upper, cap=1 << 16):
 def multi_plan(msg, lower, upper, ndev, weights=None, cap=1 << 12):
     """Host-only: how search_multi (chunk = 0) splits [lower, upper] over ndev workers with rates in
     proportion to `weights` (None = equal): head shards, then tail chunks (list of dicts)."""
+    if weights is not None and len(weights) != ndev:
+        raise ValueError(f"multi_plan: {len(weights)} weights for {ndev} workers")
     m = _b(msg)
     buf = (mh_span * cap)()
     w = None if weights is None else (ctypes.c_double * ndev)(*weights)

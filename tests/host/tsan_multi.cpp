@@ -9,7 +9,8 @@
 //     and searched by the others);
 //   * the result is the lexicographic minimum over the successful spans;
 //   * a failure returns the failing search's code and text;
-//   * rates are recorded for the devices whose searches of >= 2^30 nonces succeeded.
+//   * rates are recorded for the devices whose searches of >= 2^30 nonces succeeded;
+// and, first, that a device listed k times gets 1/k of its rate per entry (repeated_devices).
 //
 //   tsan_multi <seed> <iterations>     exit 0 = every invariant held
 #include <stdio.h>
@@ -17,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <mutex>
@@ -118,10 +120,35 @@ static void one_case(std::mt19937_64& rng, int it) {
         }
 }
 
+// A device listed k times runs its k shards one after another, so each of its entries weighs 1/k of
+// its rate and every physical device carries a share of the range in proportion to its own rate
+// (devices 10..12: never listed by one_case, so their rates are only these).
+static void repeated_devices() {
+    mh::record_rate(10, 3.0e9, 1000000000ull);  // 3 slots per ns
+    mh::record_rate(11, 3.0e9, 1000000000ull);
+    mh::record_rate(12, 1.5e9, 1000000000ull);  // half as fast
+    const int devs[5] = {10, 11, 10, 12, 10};
+    const std::vector<double> w = mh::worker_weights(devs, 5);
+    CHECK(w.size() == 5);
+    CHECK(std::abs(w[0] - 1.0) < 1e-9 && std::abs(w[2] - 1.0) < 1e-9 && std::abs(w[4] - 1.0) < 1e-9);
+    CHECK(std::abs(w[1] - 3.0) < 1e-9 && std::abs(w[3] - 1.5) < 1e-9);
+    mh::Prefix pre;
+    mh::absorb_prefix((const uint8_t*)"cmu440", 6, &pre);
+    mh::MultiPlan mp;
+    mh::multi_plan(pre, 1ull << 39, (1ull << 39) + (1ull << 34), mh::PlanOpts(), w, &mp);  // no dynamic tail
+    CHECK(mp.tail.empty());
+    double cost[3] = {0, 0, 0};
+    for (int i = 0; i < 5; ++i)
+        if (!mp.head[(size_t)i].empty)
+            cost[devs[i] - 10] += mh::segments_cost(mp.segs, mp.head[(size_t)i].lo, mp.head[(size_t)i].hi);
+    CHECK(std::abs(cost[0] / cost[1] - 1.0) < 1e-6 && std::abs(cost[2] / cost[1] - 0.5) < 1e-6);
+}
+
 int main(int argc, char** argv) {
     const uint64_t seed = argc > 1 ? strtoull(argv[1], nullptr, 10) : 440;
     const int iters = argc > 2 ? atoi(argv[2]) : 100;
     std::mt19937_64 rng(seed);
+    repeated_devices();
     for (int it = 0; it < iters; ++it) one_case(rng, it);
     printf("iterations=%d failures=%d\n", iters, g_fail);
     return g_fail ? 1 : 0;

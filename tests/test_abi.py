@@ -164,17 +164,6 @@ def test_plan_fine_tail_covers_exactly(monkeypatch):
         check_plan(m, U64 - (1 << 33), U64)
 
 
-def test_plan_finest_tail_covers_exactly(monkeypatch):
-    """MINEHIP_FINEST_TAIL (experiment): the last runs of each tail split planned once more at L - 2;
-    the plan still tiles the range exactly."""
-    monkeypatch.setenv("MINEHIP_FINEST_TAIL", str(1 << 25))
-    for m in (b"cmu440", b"x" * 60, b"a" * 100, b"y" * 52):
-        pieces = check_plan(m, 0, 2 ** 34 - 1)
-        assert [p for p in pieces if p["kind"] == 0 and p["lo_digits"] == 1 and p["count"] <= 1 << 25]
-        check_plan(m, 549755813888, 549755813888 + 6871947673)
-        check_plan(m, U64 - (1 << 33), U64)
-
-
 def test_plan_uses_fast_kernel_for_bulk():
     pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
     fast = sum(p["count"] for p in pieces if p["kind"] == 0)
@@ -317,7 +306,7 @@ def test_embedded_code_object_carries_queue_marker():
     md = codeobj.metadata(co)
     fast = [k for k in md["amdhsa.kernels"] if "fast_search" in k[".name"]]
     assert len(fast) == 22
-    assert {k[".args"][0][".size"] for k in fast} == {488}      # FastArgs, by value
+    assert {k[".args"][0][".size"] for k in fast} == {472}      # FastArgs, by value
     nomarker = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
     if os.path.exists(nomarker):
         assert b"mh_fast_queue_args" not in open(nomarker, "rb").read()

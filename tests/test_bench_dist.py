@@ -251,24 +251,31 @@ def test_rank_device_and_sharing():
 
 def test_same_workload_n1_slice_and_efficiency():
     """Every line's n1_config4_ghs is one configs[3] step -- the middle 2^40/20 slice the driver's
-    --steps 20 line runs -- searched on one device; per_gpu_efficiency = value / (N x it)
-    (VERDICT r03 next-round item 2).  The search here is a stub (no GPU)."""
+    --steps 20 line runs, rounded to whole 2^32 fixture chunks -- searched on one device;
+    per_gpu_efficiency = value / (N x it).  Its result is pinned by
+    fullsize_cfg4.json's chunk minima (golden_ok, not null).  The search here
+    is a stub (no GPU) that returns the fixture's answer for the slice."""
     calls = []
 
     def search(m, a, b):
         calls.append((m, a, b))
         time.sleep(0.01)
-        return (1, a)
+        return bench.golden_expect(m, a, b) or (1, a)
 
     r = bench.same_workload_n1(search, 20)
-    lo, hi = bench.step_range(bench.CONFIGS["4"], 10, 20)
+    lo, hi = 1 << 39, (1 << 39) + 13 * (1 << 32) - 1     # step 10 of 20 starts at 2^39; 12.8 -> 13 chunks
+    s_lo, s_hi = bench.step_range(bench.CONFIGS["4"], 10, 20)
+    assert s_lo == lo and abs((hi - lo + 1) / (s_hi - s_lo + 1) - 1) < 0.02
     assert calls[-1] == (b"cmu440", lo, hi) and r["range"] == [lo, hi]
     assert calls[0][1] == lo and calls[0][2] < hi       # the untimed warm-up search comes first
     assert 0 < r["ghs"] < (hi - lo + 1) / 0.01 / 1e9 * 1.0001
-    assert r["slice"] == "step 10 of 20"
-    # fewer steps than the driver's never makes the one-device search longer than its step
+    assert r["slice"].startswith("step 10 of 20")
+    assert bench.golden_expect(b"cmu440", lo, hi) is not None and r["golden_ok"] is True
+    assert bench.same_workload_n1(lambda m, a, b: (0, a), 20)["golden_ok"] is False
+    # fewer steps than the driver's: the driver's step; more: the middle step of those, still whole chunks
     assert bench.same_workload_n1(search, 5)["range"] == [lo, hi]
-    assert bench.same_workload_n1(search, 40)["range"] == list(bench.step_range(bench.CONFIGS["4"], 20, 40))
+    r40 = bench.same_workload_n1(search, 40)
+    assert r40["range"] == [lo, lo + 6 * (1 << 32) - 1] and r40["golden_ok"] is True
     assert bench.per_gpu_efficiency(430.0, 8, 54.0) == round(430.0 / 432.0, 4)
     assert bench.per_gpu_efficiency(54.0, 1, 54.0) == 1.0
 
@@ -293,3 +300,86 @@ def test_cpu_baseline_threads(monkeypatch):
     assert t == 1 and f["cgroup_quota_cores"] == 1
     monkeypatch.setenv("BENCH_CPU_THREADS", "3")
     assert bench.cpu_threads()[0] == 3
+
+
+# ---- the driver's N > 1 commands, on the one GPU of a test box ----------
+# The driver's scaling run is `python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`
+# (or `python bench.py --gpus N` in one process) on an 8-GPU node, once per round; a bench-only
+# regression there (r04a's TypeError in the in-process line) would cost the only 8-GPU curve.  Both
+# paths run here as fresh child processes with two workers on device 0, on configs[3] cut to
+# [0, 2^35 - 1] (fullsize_cfg2.json pins its answer), and must print one good JSON line.
+
+BENCH_N2 = ["--config", "4", "--bits", "35", "--steps", "4", "--warmup", "1", "--no-pmc", "--no-cpu-baseline"]
+
+
+def _run_group(cmd, env, timeout):
+    """Run cmd in its own process group; on a time limit kill the whole group (the launcher's ranks
+    included) and fail."""
+    import signal
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        pytest.fail(f"{' '.join(cmd[:4])}... timed out after {timeout} s\n{err[-3000:]}")
+    return p.returncode, out, err
+
+
+def _check_n2_line(line, driver):
+    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["value"] > 0
+    assert line["config"]["config"] == "4" and driver in line["config"]["driver"]
+    assert line["result"]["range"] == [0, (1 << 35) - 1]
+    assert line["result"]["golden_ok"] is True and line["result"]["rehash_ok"] is True
+    assert line["n1_config4"] and line["n1_config4"]["golden_ok"] is True and line["n1_config4_ghs"] > 0
+    assert line["per_gpu_efficiency"] is None  # --bits: not configs[3] as the driver runs it
+    assert line["roofline"]["frac"] and 0 < line["roofline"]["frac"] <= 1
+    for p in line["per_device"]:
+        assert p["dev"] == 0 and p["nonces"] > 0 and p["kernel_clock_ghz"] and 1.0 < p["kernel_clock_ghz"] <= 2.5, p
+    lo, hi = line["kernel_clock_ghz_range"]
+    assert 1.0 < lo <= hi <= 2.5
+
+
+@pytest.mark.gpu
+def test_bench_inprocess_two_workers_one_gpu():
+    """`python bench.py --gpus 2 --devices 0,0`: the in-process path (mh_search_multi, one host
+    thread per worker) with both workers on device 0; per_device has one entry per distinct device,
+    carrying its in-kernel clock read during a concurrent search."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "BENCH_DEVICE"):
+        env.pop(k, None)
+    rc, out, err = _run_group([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                               "--devices", "0,0", *BENCH_N2], env, 200)
+    assert rc == 0, err[-3000:]
+    lines = _json_lines(out)
+    assert len(lines) == 1, out[-2000:]
+    line = lines[0]
+    _check_n2_line(line, "mh_search_multi")
+    assert line["config"]["devices"] == [0, 0] and len(line["per_device"]) == 1
+    assert line["per_device"][0]["nonces"] == 1 << 35
+
+
+@pytest.mark.gpu
+def test_bench_launched_two_ranks_one_gpu():
+    """`torch.distributed.run --nproc-per-node 2 bench.py --gpus 2` (the driver's form) with both
+    ranks on device 0 (BENCH_DEVICE=0): the gloo host merge, the rate-balanced strong shards, two
+    per_device entries (one per rank, each with its clock) and ranks_per_device 2."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, BENCH_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    rc, out, err = _run_group([sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1",
+                               "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port", str(port),
+                               os.path.join(ROOT, "bench.py"), "--gpus", "2", *BENCH_N2], env, 240)
+    assert rc == 0, err[-3000:]
+    lines = _json_lines(out)
+    assert len(lines) == 1, out[-2000:]
+    line = lines[0]
+    _check_n2_line(line, "one process per GPU")
+    assert sorted(p["rank"] for p in line["per_device"]) == [0, 1]
+    assert sum(p["nonces"] for p in line["per_device"]) == 1 << 35
+    assert line["config"]["ranks_per_device"] == 2

@@ -147,9 +147,39 @@ def test_clock_probe_library_exports():
     path = os.path.join(os.path.dirname(bench.__file__), "build", "libclockprobe.so")
     lib = ctypes.CDLL(path)
     assert hasattr(lib, "cp_start") and hasattr(lib, "cp_read")
-    lib.cp_read.argtypes = [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    lib.cp_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    lib.cp_start.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
     buf = (ctypes.c_uint64 * 4)()
-    assert lib.cp_read(buf, 1) == -1            # nothing started: refused, no device touched
+    assert lib.cp_read(0, buf, 1) == -1         # nothing started: refused, no device touched
+    assert lib.cp_read(64, buf, 1) == -1        # no such device slot
+    assert lib.cp_start(-1, 0.1, 0.1, 1) == -1  # refused before any HIP call
+
+
+def test_kernel_clocks_one_thread_per_device():
+    """The in-process N-GPU line reads every device's clock at once (bench.kernel_clocks): one host
+    thread per distinct device, all probing concurrently, each with its own device's search; a
+    failing probe leaves only that device's clock unknown.  Stub probe (no GPU)."""
+    import threading
+    import time
+    seen, lock, inside = [], threading.Lock(), [0]
+    peak = [0]
+
+    def probe(search_dev, dev):
+        with lock:
+            inside[0] += 1
+            peak[0] = max(peak[0], inside[0])
+        time.sleep(0.05)
+        search_dev(b"m", dev, dev)
+        with lock:
+            inside[0] -= 1
+        if dev == 3:
+            raise RuntimeError("no clock")
+        return {"ghz": 2.0 + dev / 100}
+
+    out = bench.kernel_clocks(lambda d: (lambda m, a, b: seen.append((d, a))), [0, 1, 1, 3, 0], probe=probe)
+    assert sorted(out) == [0, 1, 3] and out[0]["ghz"] == 2.0 and out[1]["ghz"] == 2.01
+    assert out[3]["ghz"] is None and "no clock" in out[3]["note"]
+    assert sorted(seen) == [(0, 0), (1, 1), (3, 3)] and peak[0] == 3
 
 
 @pytest.mark.gpu

@@ -176,27 +176,12 @@ def test_plan_invariance_small(gpu):
                                  MINEHIP_GENERIC_BELOW=gb, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
                                  MINEHIP_QUEUE=q):
                             assert gpu.search(m, lo, hi) == exp, (m[:8], Ld, gb, st, ft, q)
-        # the finest tail on the lowest-priority stream (MINEHIP_FINEST_TAIL)
-        for ft in (1_000, 50_000):
-            with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
-                     MINEHIP_STREAMS=2, MINEHIP_FINE_TAIL=200_000, MINEHIP_FINEST_TAIL=ft):
-                assert gpu.search(m, lo, hi) == exp, (m[:8], ft)
-        # the tail split fused into the coarse launch before it (MINEHIP_FUSE_TAIL), also with tiny
-        # grids (many launches, partial-buffer flushes) and without the work queue (no fusion)
-        for fu in (0, 1):
-            for st, ft, mb, q in ((1, 20_000, 0, 1), (2, 20_000, 0, 1), (2, 200_000, 0, 1), (2, 200_000, 3, 1),
-                                  (2, 200_000, 0, 0)):
-                kv = dict(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
-                          MINEHIP_QUEUE=q, MINEHIP_FUSE_TAIL=fu)
-                if mb:
-                    kv["MINEHIP_MAX_BLOCKS"] = mb
-                with env(**kv):
-                    assert gpu.search(m, lo, hi) == exp, (m[:8], fu, st, ft, mb, q)
-        # which full-L pieces take the high-priority stream (MINEHIP_COARSE_MIN)
-        for cm in (1, 100_000, 1 << 62):
-            with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_LAUNCH_NONCES=100_000,
-                     MINEHIP_STREAMS=2, MINEHIP_COARSE_MIN=cm):
-                assert gpu.search(m, lo, hi) == exp, (m[:8], cm)
+        # the tail split on the low-priority stream with tiny grids (many launches, partial-buffer
+        # flushes on both streams)
+        for st, ft, mb, q in ((2, 200_000, 3, 1), (2, 200_000, 3, 0)):
+            with env(MINEHIP_LOWER_DIGITS=3, MINEHIP_MIN_LANES=1, MINEHIP_STREAMS=st, MINEHIP_FINE_TAIL=ft,
+                     MINEHIP_QUEUE=q, MINEHIP_MAX_BLOCKS=mb):
+                assert gpu.search(m, lo, hi) == exp, (m[:8], st, ft, mb, q)
         # tiny grids: many launches per bucket and many partial-buffer flushes (on both streams);
         # with one block per launch a search outruns the 4,096 work-queue counters, and the
         # launches past them run one workgroup per chunk
@@ -214,9 +199,8 @@ def test_full_size_properties(gpu, msg, bits):
     hi = (1 << bits) - 1
     r = gpu.search(msg, 0, hi)
     assert oracle.hash_(msg, r[1]) == r[0] and 0 <= r[1] <= hi  # re-hashes to itself
-    for fu in (0, 1):  # tail splits in launches of their own / fused into the coarse launches
-        with env(MINEHIP_FUSE_TAIL=fu):
-            assert gpu.search(msg, 0, hi) == r, fu
+    with env(MINEHIP_STREAMS=1, MINEHIP_FINE_TAIL=0):  # one stream, no tail split
+        assert gpu.search(msg, 0, hi) == r
     rng = random.Random(bits)
     for _ in range(2):  # split-range associativity
         mid = rng.randrange(1, hi)

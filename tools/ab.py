@@ -12,7 +12,8 @@ Recipe (JSON):
   {"about": "...", "tag": "r03u",
    "variants": {"name": "K=V,K=V" | "", ...},          # "" = the product build as is
    "code_objects": {"name": "build/ab/x.hsaco"},       # shorthand: MINEHIP_DEV_CODE_OBJECT=...
-   "workloads": [["d10", 7, "clock"], ["cfg1", 9], ...]}  # WORKLOADS name, rounds, optional clock
+   "workloads": [["d10", 7, "clock"], ["cfg1", 9], ...],  # WORKLOADS name, rounds, optional clock
+   "retired": "why"}   # optional: the knobs it varies left the library; kept as the record, not run
 The recipes under tools/ab/ are the experiments behind DESIGN.md and profiles/ (HISTORY.md).
 """
 import argparse
@@ -82,6 +83,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true")
     a = ap.parse_args()
     recipe, variants = load(a.recipe)
+    if recipe.get("retired") and not a.dry_run:
+        raise SystemExit(f"{a.recipe}: retired ({recipe['retired']})")
     out = os.path.join(ROOT, "gpurun_out", a.tag or recipe.get("tag", "ab"))
     cmds = commands(recipe, variants, set(a.only.split(",")) if a.only else None)
     if a.dry_run:

@@ -12,10 +12,13 @@
 // slot on a few SIMDs from the search.  Results go to a buffer of their own by vector stores.
 //
 // C-ABI (build/libclockprobe.so, loaded by bench.py with ctypes; measurement only):
-//   cp_start(dev, delay_s, window_s, nwg)  launch nwg probe workgroups, return at once
-//   cp_read(out, nwg)                      wait for them; out[4*i..4*i+3] = {xcc, cycles,
+//   cp_start(dev, delay_s, window_s, nwg)  launch nwg probe workgroups on device dev, return at once
+//   cp_read(dev, out, nwg)                 wait for them; out[4*i..4*i+3] = {xcc, cycles,
 //                                          100 MHz ticks, ticks from the workgroup's start to
 //                                          its window}
+// One probe at a time per device; probes on different devices may run at once, each started and
+// read from its own host thread (bench.py's in-process N-GPU lines read every device's clock
+// during concurrent searches).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -48,47 +51,53 @@ __global__ void clock_probe(uint64_t* __restrict__ out, uint64_t delay_ticks, ui
     }
 }
 
-hipStream_t g_stream = nullptr;
-uint64_t* g_out = nullptr;
-int g_nwg = 0;
-int g_dev = -1;
+constexpr int kMaxDevices = 64;
+struct Slot {
+    hipStream_t stream = nullptr;  // created on the slot's device
+    uint64_t* out = nullptr;       // non-null while a probe is outstanding
+    int nwg = 0;
+};
+Slot g_slot[kMaxDevices];  // slot d is touched only by the thread that probes device d
 
 }  // namespace
 
 extern "C" int cp_start(int dev, double delay_s, double window_s, int nwg) {
-    if (nwg < 1 || nwg > 4096 || delay_s < 0 || window_s <= 0 || g_out) return -1;
+    if (dev < 0 || dev >= kMaxDevices) return -1;
+    Slot& s = g_slot[dev];
+    if (nwg < 1 || nwg > 4096 || delay_s < 0 || window_s <= 0 || s.out) return -1;
     if (hipSetDevice(dev) != hipSuccess) return -2;
-    if (!g_stream && hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess) return -3;
-    if (hipMalloc(&g_out, sizeof(uint64_t) * 4 * nwg) != hipSuccess) {
-        g_out = nullptr;
+    if (!s.stream && hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) return -3;
+    if (hipMalloc(&s.out, sizeof(uint64_t) * 4 * nwg) != hipSuccess) {
+        s.out = nullptr;
         return -4;
     }
-    if (hipMemsetAsync(g_out, 0, sizeof(uint64_t) * 4 * nwg, g_stream) != hipSuccess) {
-        (void)hipFree(g_out);
-        g_out = nullptr;
+    if (hipMemsetAsync(s.out, 0, sizeof(uint64_t) * 4 * nwg, s.stream) != hipSuccess) {
+        (void)hipFree(s.out);
+        s.out = nullptr;
         return -5;
     }
-    g_nwg = nwg;
-    g_dev = dev;
-    hipLaunchKernelGGL(clock_probe, dim3(nwg), dim3(64), 0, g_stream, g_out,
+    s.nwg = nwg;
+    hipLaunchKernelGGL(clock_probe, dim3(nwg), dim3(64), 0, s.stream, s.out,
                        (uint64_t)(delay_s * kRealtimeHz), (uint64_t)(window_s * kRealtimeHz));
     if (hipGetLastError() != hipSuccess) {  // nothing runs: free the buffer so a later start works
-        (void)hipStreamSynchronize(g_stream);
-        (void)hipFree(g_out);
-        g_out = nullptr;
+        (void)hipStreamSynchronize(s.stream);
+        (void)hipFree(s.out);
+        s.out = nullptr;
         return -6;
     }
     return 0;
 }
 
-extern "C" int cp_read(uint64_t* out, int nwg) {
-    if (!g_out || nwg != g_nwg) return -1;
-    if (hipSetDevice(g_dev) != hipSuccess) return -2;
+extern "C" int cp_read(int dev, uint64_t* out, int nwg) {
+    if (dev < 0 || dev >= kMaxDevices) return -1;
+    Slot& s = g_slot[dev];
+    if (!s.out || nwg != s.nwg) return -1;
+    if (hipSetDevice(dev) != hipSuccess) return -2;
     int rc = 0;
-    if (hipStreamSynchronize(g_stream) != hipSuccess ||
-        hipMemcpy(out, g_out, sizeof(uint64_t) * 4 * nwg, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipStreamSynchronize(s.stream) != hipSuccess ||
+        hipMemcpy(out, s.out, sizeof(uint64_t) * 4 * nwg, hipMemcpyDeviceToHost) != hipSuccess)
         rc = -3;
-    (void)hipFree(g_out);
-    g_out = nullptr;
+    (void)hipFree(s.out);
+    s.out = nullptr;
     return rc;
 }
