@@ -42,7 +42,7 @@ for s in $STEPS; do
       newer=$(find "$ROOT/bitcoin-miner_amd/csrc" "$ROOT/include" -newer "$ROOT/bitcoin-miner_amd/minehip/libminehip.so" \
               \( -name '*.hip' -o -name '*.cpp' -o -name '*.hpp' -o -name '*.h' -o -name '*.py' \) | head -3)
       [ -z "$newer" ] || echo "WARNING: sources newer than libminehip.so: $newer" | tee -a "$OUT/session.log"
-      timeout -k 10 900 python -u -m pytest "$ROOT/tests" -m gpu -v -x -p no:cacheprovider --timeout 150 \
+      timeout -k 10 900 python -u -m pytest "$ROOT/tests" -m gpu -v -x -p no:cacheprovider --durations=25 --timeout 150 \
           --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/session.log"; tail -3 "$OUT/pytest_gpu.log"; fatal $rc
       ;;
