@@ -709,7 +709,7 @@ def roofline(kst, cus, n_devices, resources=None, loop_mix=None):
     if not kst:
         return {"bound": "valu", "achieved": None, "peak": round(peak, 3), "frac": None}
     dom = kst[0]
-    blocks = 1 if dom["mode"] == 0 else 2       # tail blocks hashed per nonce (Pre/Two: 2)
+    blocks = 1 if dom["mode"] % 3 == 0 else 2   # tail blocks hashed per nonce (Pre/Two and their Early modes: 2)
     sec = dom["ns"] * 1e-9
     nonces = max(1, dom["nonces"])
     ghs = dom["nonces"] / sec / 1e9

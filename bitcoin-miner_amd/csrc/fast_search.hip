@@ -27,13 +27,14 @@
 // occupancy the layout reaches as a one-chunk-per-workgroup kernel (VGPRs 59..79 -> 7 or 6 waves,
 // the Two layouts 98..110 -> 4).  The work-queue loop around the chunk body would otherwise let
 // the allocator take 4..6 more VGPRs and cost a wave per SIMD.  -DMH_MIN_WAVES=n overrides all.
+// The Early modes (layout.hpp) take the occupancy of their tail layout.
 constexpr int min_waves(int J, int MODE) {
 #ifdef MH_MIN_WAVES
     return MH_MIN_WAVES;
 #else
-    return MODE == 2 ? 4
-         : MODE == 1 ? ((J == 0 || J == 4) ? 6 : 7)
-                     : ((J == 7 || J == 8 || J >= 10) ? 6 : 7);
+    return MODE % 3 == 2 ? 4
+         : MODE % 3 == 1 ? ((J == 0 || J == 4) ? 6 : 7)
+                         : ((J == 7 || J == 8 || J >= 10) ? 6 : 7);
 #endif
 }
 
@@ -42,12 +43,13 @@ namespace mh {
 // ---------------------------------------------------------------------------
 // fast_search<J, MODE>
 // ---------------------------------------------------------------------------
-// Inside a lane only message word J (the last digit's word) changes from one
-// nonce to the next, and word J-1 changes once per group of 10 nonces.  Every
+// Inside a lane only message word J (the last digit's word; Early modes: the
+// word the innermost digit ends) changes from one nonce to the next, and word
+// J-1 (Early: J+1) changes once per group of 10 nonces.  Every
 // schedule word W[t] therefore lives at one of three levels, fixed at compile
 // time by J:
 //   nonce  depends on W[J]                    -> computed per nonce
-//   group  depends on W[J-1] but not on W[J]  -> once per 10 nonces
+//   group  depends on W[J-1] (Early: W[J+1]) but not on W[J] -> once per 10 nonces
 //   run    neither                            -> once per lane (10^L nonces)
 // and each per-nonce / per-group word is split into its cheaper-level partial
 // sum plus the terms of its own level.  Words after J hold only padding and
@@ -117,15 +119,37 @@ __device__ __forceinline__ void sha256_block_kw_last(const uint32_t st[8], const
 }
 }  // namespace dev
 
+// spread(x, k) = x with a zero decimal digit inserted at digit index k (k >= 20: x itself), by
+// divisions by the constant 10 (no general 64-bit division); on the rare new-best branch of the
+// Early modes only
+__device__ __forceinline__ uint64_t spread(uint64_t x, uint32_t k) {
+    if (k >= 20u) return x;
+    uint64_t lo = 0, p = 1;
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t q = x / 10u;
+        lo += (x - q * 10u) * p;
+        p *= 10u;
+        x = q;
+    }
+    return x * p * 10u + lo;
+}
+
 // One workgroup-sized chunk: the 256 runs u_start + 256 * blk + threadIdx.x, their minimum
 // written to partials[blk].
+// MODE % 3 is the tail layout (One, Pre, Two); MODE >= 3 (Early): the per-nonce digit ends word
+// J and the group digits lie in words J and J + 1, so word J + 1 is the group-level word and
+// rounds 0..J-1 are all run-level; otherwise the per-nonce digit is the last one (word J) and
+// the group digits lie in words J - 1 and J.
 template <int J, int MODE>
 __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restrict__ partials, const uint32_t blk) {
     using namespace dev;
     constexpr uint32_t K[64] = MH_K256;
-    constexpr uint64_t NM = Dep::from(J);               // nonce-level words
-    constexpr uint64_t GM = Dep::from(J - 1) & ~NM;     // group-level words
-    constexpr int BASE = (MODE == kModePre) ? 16 : 0;   // per-nonce block inside the tail
+    constexpr int BM = MODE % 3;                          // tail layout
+    constexpr bool EARLY = MODE >= 3;
+    constexpr int JG = EARLY ? J + 1 : J - 1;             // the other word of the group digits
+    constexpr uint64_t NM = Dep::from(J);                 // nonce-level words
+    constexpr uint64_t GM = Dep::from(JG) & ~NM;          // group-level words
+    constexpr int BASE = (BM == kModePre) ? 16 : 0;       // per-nonce block inside the tail
 #define MH_N(t) ((NM >> (t)) & 1ull)
 #define MH_G(t) ((GM >> (t)) & 1ull)
 #define MH_R(t) (!MH_N(t) && !MH_G(t))
@@ -134,9 +158,11 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
 
     // ---- per run --------------------------------------------------------
     // Tail words: host template + the d-L digits of U, right-aligned so U's
-    // last digit sits at tail byte hi_end-1.  Only words before the lower
-    // digits can receive them (words < BASE + J).
-    constexpr int NW = BASE + J + 1;
+    // last digit sits at tail byte hi_end-1 (Early: skipping the innermost
+    // digit's byte).  Only words up to the last lower digit's can receive them
+    // (words <= BASE + J, Early BASE + J + 1).
+    constexpr int JM = EARLY ? J + 1 : J;                 // the last per-lane word
+    constexpr int NW = BASE + JM + 1;
     uint32_t w[NW];
 #pragma unroll
     for (int x = 0; x < NW; ++x) w[x] = a.blk[x];
@@ -148,29 +174,30 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
                 const uint64_t q = u / 10u;
                 const uint32_t dg = (uint32_t)(u - q * 10u);
                 u = q;
-                const uint32_t pos = a.hi_end - 1u - (uint32_t)k;
+                uint32_t pos = a.hi_end - 1u - (uint32_t)k;
+                if constexpr (EARLY) pos -= ((uint32_t)k >= a.hole) ? 1u : 0u;
                 add_word(w, pos >> 2, dg << (24u - 8u * (pos & 3u)));
             }
         }
     }
-    // words of the per-nonce block: per-lane up to J, uniform (SGPR) after J
+    // words of the per-nonce block: per-lane up to JM, uniform (SGPR) after it
     uint32_t W[16];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) W[t] = (t <= J) ? w[BASE + t] : a.blk[BASE + t];
+    for (int t = 0; t < 16; ++t) W[t] = (t <= JM) ? w[BASE + t] : a.blk[BASE + t];
 
     uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) st[i] = a.mid[i];
-    if constexpr (MODE == kModePre) {
+    if constexpr (BM == kModePre) {
         uint32_t b0[16];
 #pragma unroll
         for (int t = 0; t < 16; ++t) b0[t] = w[t];
         sha256_block(st, b0);  // tail block 0 holds no lower digit: once per run
     }
-    // rounds 0..J-2 read only run-level words
+    // rounds 0..J-2 (Early: 0..J-1) read only run-level words
     uint32_t ra = st[0], rb = st[1], rc = st[2], rd = st[3], re = st[4], rf = st[5], rg = st[6], rh = st[7];
 #pragma unroll
-    for (int t = 0; t + 1 < J; ++t) round_kw(ra, rb, rc, rd, re, rf, rg, rh, K[t] + W[t]);
+    for (int t = 0; t < (EARLY ? J : J - 1); ++t) round_kw(ra, rb, rc, rd, re, rf, rg, rh, K[t] + W[t]);
 
     // run-level schedule words, and the run-level part of the others
     uint32_t wr[64], pr[64];
@@ -197,7 +224,8 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
             asm volatile("" : "+v"(kwr[t]));
         }
 
-    const uint32_t lastpos = a.lo_pos + a.L - 1u;  // byte of the last digit, in word J
+    // byte of the per-nonce digit, in word J: the last digit, or (Early) the innermost one
+    const uint32_t lastpos = EARLY ? a.inner : a.lo_pos + a.L - 1u;
     const uint32_t sh_last = 24u - 8u * (lastpos & 3u);
     // The best (H0, H1, nonce) of the whole wave so far, wave-uniform (SGPRs).
     // A lane is a candidate when its H0 <= the wave's best H0: the compare is
@@ -214,23 +242,41 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
 
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
-        // digits 0..L-2 of q = 10*g + i: wave-uniform, so this is SALU work
+        // the L-1 digits of g: wave-uniform, so this is SALU work.  Into word J (cj) or the
+        // other group word JG (cjm)
         uint32_t cj = 0u, cjm = 0u, gq = g;
-        for (uint32_t k = a.L - 1u; k-- > 0u;) {
-            const uint32_t q = gq / 10u;
-            const uint32_t dg = gq - q * 10u;
-            gq = q;
-            const uint32_t p = a.lo_pos + k;
-            const uint32_t v = dg << (24u - 8u * (p & 3u));
-            if ((p >> 2) == (uint32_t)J)
-                cj += v;
-            else
-                cjm += v;
+        if constexpr (!EARLY) {
+            // digits 0..L-2 of q = 10*g + i, at bytes lo_pos .. lo_pos+L-2
+            for (uint32_t k = a.L - 1u; k-- > 0u;) {
+                const uint32_t q = gq / 10u;
+                const uint32_t dg = gq - q * 10u;
+                gq = q;
+                const uint32_t p = a.lo_pos + k;
+                const uint32_t v = dg << (24u - 8u * (p & 3u));
+                if ((p >> 2) == (uint32_t)J)
+                    cj += v;
+                else
+                    cjm += v;
+            }
+        } else {
+            // g's digit j (least significant first) at byte g_last - j, one more to the left
+            // from j = g_hole on (the innermost digit's decimal place)
+            for (uint32_t j = 0; j + 1u < a.L; ++j) {
+                const uint32_t q = gq / 10u;
+                const uint32_t dg = gq - q * 10u;
+                gq = q;
+                const uint32_t p = a.g_last - j - (j >= a.g_hole ? 1u : 0u);
+                const uint32_t v = dg << (24u - 8u * (p & 3u));
+                if ((p >> 2) == (uint32_t)J)
+                    cj += v;
+                else
+                    cjm += v;
+            }
         }
-        const uint32_t wJ = W[J] + cj;  // word J with this group's digits, last digit '0'
+        const uint32_t wJ = W[J] + cj;  // word J with this group's digits, the per-nonce digit '0'
         const uint32_t s0wJ = ssig0(wJ), s1wJ = ssig1(wJ);
         uint32_t wg[64], pg[64];
-        if constexpr (J > 0) wg[J - 1] = W[J - 1] + cjm;
+        if constexpr (JG >= 0) wg[JG] = W[JG] + cjm;
 #pragma unroll
         for (int t = 16; t < 64; ++t) {
             if (MH_R(t)) continue;
@@ -241,9 +287,9 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
             if (MH_G(t - 2)) v += ssig1(wg[t - 2]);
             if (MH_G(t)) wg[t] = v; else pg[t] = v;
         }
-        // round J-1 reads the group-level word J-1
+        // round J-1 reads the group-level word J-1 (Early: it is run-level, done above)
         uint32_t ga = ra, gb = rb, gc = rc, gd = rd, ge = re, gf = rf, gG = rg, gh = rh;
-        if constexpr (J > 0) round_kw(ga, gb, gc, gd, ge, gf, gG, gh, K[J - 1] + wg[J - 1]);
+        if constexpr (!EARLY && J > 0) round_kw(ga, gb, gc, gd, ge, gf, gG, gh, K[J - 1] + wg[J - 1]);
         // round J: every input but W[J]'s last digit is known here
         const uint32_t t1J = (gh + (K[J] + wJ)) + bsig1(ge) + ch(ge, gf, gG);
         const uint32_t t2J = bsig0(ga) + maj(ga, gb, gc);
@@ -270,7 +316,7 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
             const uint32_t t1 = t1J + inc;
             uint32_t A = t1 + t2J, B = ga, C = gb, D = gc, E = gd + t1, F = ge, G = gf, H = gG;
             uint32_t h0, a63;
-            if constexpr (MODE != kModeTwo) {
+            if constexpr (BM != kModeTwo) {
 #pragma unroll
                 for (int t = J + 1; t < 63; ++t) {
                     sched(t);
@@ -313,7 +359,11 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
                     m &= m - 1ull;
                     const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)h0, (int)l);
                     const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)h1, (int)l);
-                    const uint64_t cn = (wave_u0 + l) * a.pow10L + q;
+                    uint64_t cn;
+                    if constexpr (!EARLY)
+                        cn = (wave_u0 + l) * a.pow10L + q;
+                    else
+                        cn = spread(wave_u0 + l, a.hole) * a.u_mul + spread(g, a.g_hole) + i * a.i_mul;
                     if (c0 < wbh0 || (c0 == wbh0 && (c1 < wbh1 || (c1 == wbh1 && cn < wbn)))) {
                         wbh0 = c0;
                         wbh1 = c1;
@@ -377,13 +427,16 @@ __device__ __attribute__((used)) uint8_t mh_fast_queue_args[sizeof(FastArgs)];
 // The instantiations the planner uses (plan.cpp; launch by mangled name in
 // search_kernels.hip): kModeOne for every word J of the last digit in a
 // one-block tail, kModePre for J <= 4 of block 1 (last digit at tail byte
-// 64..82), kModeTwo for J = 13..15 of block 0.
+// 64..82), kModeTwo for J = 13..15 of block 0; the Early modes where a nonce
+// costs less with the digit ending word J innermost than with the last digit
+// in word J + 1 (plan.cpp: nonce_cost(J) < nonce_cost(J + 1)).
 #define MH_INST(j, m) template __global__ void fast_search<j, m>(const FastArgs, Partial* __restrict__);
 MH_INST(0, kModeOne) MH_INST(1, kModeOne) MH_INST(2, kModeOne) MH_INST(3, kModeOne) MH_INST(4, kModeOne)
 MH_INST(5, kModeOne) MH_INST(6, kModeOne) MH_INST(7, kModeOne) MH_INST(8, kModeOne) MH_INST(9, kModeOne)
 MH_INST(10, kModeOne) MH_INST(11, kModeOne) MH_INST(12, kModeOne) MH_INST(13, kModeOne)
 MH_INST(0, kModePre) MH_INST(1, kModePre) MH_INST(2, kModePre) MH_INST(3, kModePre) MH_INST(4, kModePre)
 MH_INST(13, kModeTwo) MH_INST(14, kModeTwo) MH_INST(15, kModeTwo)
+MH_INST(0, kModeOneEarly) MH_INST(8, kModeOneEarly) MH_INST(0, kModePreEarly) MH_INST(13, kModeTwoEarly)
 #undef MH_INST
 
 }  // namespace mh

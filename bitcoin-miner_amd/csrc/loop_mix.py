@@ -78,8 +78,8 @@ def loop_mix(text):
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     mix = loop_mix(open(src).read())
-    if len(mix) != 22 or any(v["valu"] == 0 for v in mix.values()):
-        sys.exit(f"loop_mix: expected 22 fast_search loops in {src}, found {len(mix)}")
+    if len(mix) != 26 or any(v["valu"] == 0 for v in mix.values()):
+        sys.exit(f"loop_mix: expected 26 fast_search loops in {src}, found {len(mix)}")
     with open(dst, "w") as f:
         json.dump(mix, f, indent=0, sort_keys=True)
     print(f"loop_mix: {len(mix)} per-nonce loops -> {dst}")

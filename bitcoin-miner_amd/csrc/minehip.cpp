@@ -75,8 +75,8 @@ struct Timed {
 struct VarStat {
     uint64_t launches = 0, nonces = 0, ns = 0, ops = 0, slots = 0;
 };
-constexpr int kVariants = 16 * 3 * 5;  // J < 16, mode < 3, L = 1..5
-inline int var_index(int J, int mode, int L) { return J + 16 * mode + 48 * (L - 1); }
+constexpr int kVariants = 16 * mh::kModes * 5;  // J < 16, mode < kModes, L = 1..5
+inline int var_index(int J, int mode, int L) { return J + 16 * mode + 16 * mh::kModes * (L - 1); }
 
 struct DevCtx {
     std::mutex mu;
@@ -286,6 +286,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //                          2^28; 0: none)
 //   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
 //                          XCDs take more; default); 0: one workgroup per chunk
+//   MINEHIP_EARLY          1: the Early layouts where a nonce costs less with the digit ending the
+//                          word before the last digit's innermost (default); 0: never
 mh::PlanOpts plan_opts() {
     mh::PlanOpts o;
     if (const char* e = getenv("MINEHIP_LOWER_DIGITS")) {
@@ -310,6 +312,10 @@ mh::PlanOpts plan_opts() {
     if (const char* e = getenv("MINEHIP_QUEUE")) {
         const int v = atoi(e);
         if (v == 0 || v == 1) o.queue = v;
+    }
+    if (const char* e = getenv("MINEHIP_EARLY")) {
+        const int v = atoi(e);
+        if (v == 0 || v == 1) o.early = v;
     }
     return o;
 }
@@ -604,8 +610,8 @@ int mh_profile_kernels(int dev, mh_kernel_stat* out, int cap) {
         if (!v.launches) continue;
         if (n < cap) {
             out[n].word = i % 16;
-            out[n].mode = (i / 16) % 3;
-            out[n].lo_digits = i / 48 + 1;
+            out[n].mode = (i / 16) % mh::kModes;
+            out[n].lo_digits = i / (16 * mh::kModes) + 1;
             out[n].reserved = 0;
             out[n].launches = v.launches;
             out[n].nonces = v.nonces;

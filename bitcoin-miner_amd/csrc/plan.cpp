@@ -146,7 +146,7 @@ NonceCost nonce_cost(int J, int mode) {
         ops += inv_h ? 13u : 14u;
         slots += 16u + (inv_h ? 5u : inv_w ? 6u : 7u);
     }
-    if (mode == kModeTwo) {
+    if (mode % 3 == kModeTwo) {
         ops += 8u;                   // feed-forward into block 1
         slots += 8u;
         ops += 64u * 14u - 1u;       // block 1: schedule host-known, no e' in its last round;
@@ -165,8 +165,25 @@ uint32_t nonce_ops(int J, int mode) { return nonce_cost(J, mode).ops; }
 
 namespace {
 
-// Fast-kernel launch template for bucket d with L lower digits.
-bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, int* blocks_out, FastArgs* fa) {
+// The instantiated fast kernels (fast_search.hip; search_kernels.hip fast_variant_exists).
+bool kernel_exists(int J, int mode) {
+    switch (mode) {
+        case kModeOne: return J >= 0 && J <= 13;
+        case kModePre: return J >= 0 && J <= 4;
+        case kModeTwo: return J >= 13 && J <= 15;
+        case kModeOneEarly: return J == 0 || J == 8;
+        case kModePreEarly: return J == 0;
+        case kModeTwoEarly: return J == 13;
+        default: return false;
+    }
+}
+
+// Fast-kernel launch template for bucket d with L lower digits.  early: the digit ending the word
+// before the last digit's is enumerated innermost (layout.hpp kMode*Early) -- false when the
+// layout does not allow it.  *block_out: the nonces of one block of lanes (10^L, or 10^(p+1)
+// when the innermost digit sits at decimal position p >= L), the unit a piece is cut in.
+bool make_fast_args(const Prefix& pre, int d, int L, bool early, int* J_out, int* mode_out, int* blocks_out,
+                    uint64_t* block_out, FastArgs* fa) {
     const uint32_t t = pre.t;
     const uint32_t total = t + (uint32_t)d;
     const int nb = (total + 9u <= 64u) ? 1 : 2;
@@ -185,10 +202,25 @@ bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, 
         base = 0;
     }
     const uint32_t lo = pl - (uint32_t)L + 1u - base;  // first lower digit, per-nonce-block relative
-    const int J = (int)((pl - base) >> 2);
-    if ((int)(lo >> 2) < J - 1) return false;  // lower digits must span words J-1..J only
-    // the instantiated kernels (search_kernels.hip launch_fast)
-    if (mode == kModeTwo ? (J < 13 || J > 15) : (J < 0 || J > (mode == kModePre ? 4 : 13))) return false;
+    int J = (int)((pl - base) >> 2);
+    uint32_t p = 0, ib = 0;  // early: the innermost digit's decimal position and tail byte
+    if (!early) {
+        if ((int)(lo >> 2) < J - 1) return false;  // lower digits must span words J-1..J only
+    } else {
+        if (J < 1) return false;
+        ib = base + 4u * (uint32_t)J - 1u;  // the byte ending word J - 1
+        if (ib < t || ib < base) return false;  // no digit there, or not in the per-nonce block
+        p = pl - ib;
+        if (p < 1u || p >= (uint32_t)d) return false;
+        // the group digits (the L-1 lowest positions other than p) in words J-1 and J
+        for (uint32_t j = 0; j + 1u < (uint32_t)L; ++j) {
+            const uint32_t pos = j + ((p < (uint32_t)L && j >= p) ? 1u : 0u);
+            if (pl - pos < base || (int)((pl - pos - base) >> 2) < J - 1) return false;
+        }
+        J -= 1;
+        mode += 3;
+    }
+    if (!kernel_exists(J, mode)) return false;
 
     memset(fa, 0, sizeof *fa);
     memcpy(fa->mid, pre.mid, sizeof pre.mid);
@@ -206,7 +238,26 @@ bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, 
     fa->L = (uint32_t)L;
     fa->n_groups = (uint32_t)kPow10[L - 1];
     fa->mode = (uint32_t)mode;
-    if (mode == kModeTwo) {
+    fa->hole = kNoHole;
+    fa->g_hole = kNoHole;
+    uint64_t block = kPow10[L];
+    if (early) {
+        // positions 0..L-2 other than p: the group; the rest, p excluded: U, from the lowest
+        fa->inner = ib - base;
+        fa->g_last = pl - base;
+        fa->i_mul = kPow10[p];
+        if (p < (uint32_t)L) {  // contiguous lanes: U at positions L.., the group around p
+            fa->g_hole = p;
+            fa->u_mul = kPow10[L];
+        } else {                // U at positions L-1.. skipping p: lanes of one block interleave
+            fa->hi_end = total - (uint32_t)L + 1u;
+            fa->hole = p - (uint32_t)(L - 1);
+            fa->u_mul = kPow10[L - 1];
+            block = kPow10[p + 1u];
+        }
+    }
+    *block_out = block;
+    if (mode % 3 == kModeTwo) {
         uint32_t w[64];
         schedule(fa->blk + 16, w);
         for (int i = 0; i < 64; ++i) fa->kw1[i] = kK[i] + w[i];
@@ -217,17 +268,40 @@ bool make_fast_args(const Prefix& pre, int d, int L, int* J_out, int* mode_out, 
     return true;
 }
 
+// The layout of bucket d's nonces [A, B] at L lower digits: the last digit innermost, or (opt.early)
+// the digit ending the word before the last digit's, when that makes a nonce cheaper and the range
+// still holds two blocks of its lanes.  False when no fast kernel takes the bucket at this L.
+bool pick_layout(const Prefix& pre, int d, int L, uint64_t A, uint64_t B, const PlanOpts& opt, int* J, int* mode,
+                 int* nb, uint64_t* block, FastArgs* fa) {
+    if (!make_fast_args(pre, d, L, false, J, mode, nb, block, fa)) return false;
+    if (opt.early) {
+        int Je, me, nbe;
+        uint64_t be;
+        FastArgs fe;
+        if (make_fast_args(pre, d, L, true, &Je, &me, &nbe, &be, &fe) &&
+            nonce_cost(Je, me).slots < nonce_cost(*J, *mode).slots && B - A >= 2u * be) {
+            *J = Je;
+            *mode = me;
+            *nb = nbe;
+            *block = be;
+            *fa = fe;
+        }
+    }
+    return true;
+}
+
 // The fast layout of bucket d's nonces [A, B] (A <= B, all of [lower, upper] that lies in the
-// bucket): L as the planner picks it, or false when the bucket goes to the generic kernel.
+// bucket): L as the planner picks it and its layout (pick_layout), or false when the bucket goes
+// to the generic kernel.
 bool bucket_layout(const Prefix& pre, int d, uint64_t A, uint64_t B, const PlanOpts& opt, int* L_out, int* J,
-                   int* mode, int* nb, FastArgs* fa) {
+                   int* mode, int* nb, uint64_t* block, FastArgs* fa) {
     int L = std::min(opt.lower_digits, d - 1);
     L = std::min(L, 5);
     // A lane runs 10^L nonces serially: a bucket with few runs would leave
     // most SIMDs idle and end in a long tail, so shorten the runs until
     // the bucket has min_lanes of them (2^19: ~8 workgroups per CU, one generation of the grid).
     while (L > 1 && (B - A) / kPow10[L] + 1u < opt.min_lanes) --L;
-    while (L >= 1 && !make_fast_args(pre, d, L, J, mode, nb, fa)) --L;
+    while (L >= 1 && !pick_layout(pre, d, L, A, B, opt, J, mode, nb, block, fa)) --L;
     *L_out = L;
     return L >= 1 && B - A >= opt.generic_below;
 }
@@ -244,10 +318,11 @@ void cost_segments(const Prefix& pre, uint64_t lower, uint64_t upper, const Plan
     for (int d = d_lo; d <= d_hi; ++d) {
         const uint64_t A = std::max(lower, bucket_lo(d)), B = std::min(upper, bucket_hi(d));
         int L = 0, J = 0, mode = 0, nb = 1;
+        uint64_t blk = 1;
         FastArgs fa;
         double per;
         bool steady = false;
-        if (bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &fa)) {
+        if (bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &blk, &fa)) {
             steady = L == opt.lower_digits && (B - A) / kPow10[L] + 1u >= (1u << 21);
             // the fast kernel's issue slots per nonce, plus the per-run / per-group work that shorter
             // lanes amortise over fewer nonces (L = 2: ~3%, L = 1: ~6% per nonce)
@@ -380,13 +455,16 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const uint64_t A = std::max(lower, bucket_lo(d)), B = std::min(upper, bucket_hi(d));
         FastArgs fa;
         int L = 0, J = 0, mode = 0, nb = 1;
-        if (!bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &fa)) {
+        uint64_t blk = 1;
+        if (!bucket_layout(pre, d, A, B, opt, &L, &J, &mode, &nb, &blk, &fa)) {
             if (!emit_generic(A, B, d)) return;
             continue;
         }
-        const unsigned __int128 R = kPow10[L];
+        // whole blocks of lanes: a block is one run of 10^L nonces, or (an Early layout with the
+        // innermost digit at position p >= L) the 10^(p+1) nonces its 10^(p+1-L) lanes interleave
+        const unsigned __int128 R = blk;
         const unsigned __int128 U0 = ((unsigned __int128)A + R - 1u) / R;
-        const unsigned __int128 U1p = ((unsigned __int128)B + 1u) / R;  // one past the last full run
+        const unsigned __int128 U1p = ((unsigned __int128)B + 1u) / R;  // one past the last full block
         if (U0 >= U1p) {
             if (!emit_generic(A, B, d)) return;
             continue;
@@ -397,21 +475,27 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         if (!flush_generic()) return;
         // Tail split (opt.fine_tail): the last runs of a full-L bucket at L - 1, so that their
         // short workgroups can back-fill the drain of the coarse launches (streams = 2).
-        unsigned __int128 U_split = U1p;  // coarse runs [U0, U_split), then the tail at L - 1
+        unsigned __int128 U_split = U1p;  // coarse blocks [U0, U_split), then the tail at L - 1
         int Lf = 0, Jf = 0, modef = 0, nbf = 1;
+        uint64_t blkf = 1;
         FastArgs faf;
         if (opt.fine_tail && L == opt.lower_digits && L >= 2) {
-            const unsigned __int128 tail_runs = opt.fine_tail / (uint64_t)R;
-            if (tail_runs >= 1 && (U1p - U0) > 4 * tail_runs && make_fast_args(pre, d, L - 1, &Jf, &modef, &nbf, &faf)) {
-                U_split = U1p - tail_runs;
+            const unsigned __int128 tail_blocks = opt.fine_tail / (uint64_t)R;
+            if (tail_blocks >= 1 && (U1p - U0) > 4 * tail_blocks &&
+                pick_layout(pre, d, L - 1, A, B, opt, &Jf, &modef, &nbf, &blkf, &faf) && R % blkf == 0u) {
+                U_split = U1p - tail_blocks;
                 Lf = L - 1;
             }
         }
-        auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, int Lx, int Jx, int modex, int nbx,
-                             const FastArgs& fax) -> bool {  // runs [ua, ub) of 10^Lx nonces
+        // blocks [ua, ub) of Bx nonces, each 10^Lx-nonce lanes [ua * lpb, ub * lpb)
+        auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, uint64_t Bx, int Lx, int Jx, int modex,
+                             int nbx, const FastArgs& fax) -> bool {
             const unsigned __int128 Rx = kPow10[Lx];
-            const uint64_t max_runs =
-                std::max<uint64_t>(1u, std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx));
+            const uint64_t lpb = Bx / (uint64_t)Rx;  // lanes per block
+            uint64_t max_runs = std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx);
+            max_runs = std::max<uint64_t>(lpb, max_runs / lpb * lpb);  // whole blocks per launch
+            ua *= lpb;
+            ub *= lpb;
             for (unsigned __int128 u = ua; u < ub;) {
                 const unsigned __int128 left = ub - u;
                 const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
@@ -435,8 +519,9 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             }
             return true;
         };
-        if (!emit_runs(U0, U_split, L, J, mode, nb, fa)) return;
-        if (U_split < U1p && !emit_runs(U_split * 10u, U1p * 10u, Lf, Jf, modef, nbf, faf)) return;
+        if (!emit_runs(U0, U_split, blk, L, J, mode, nb, fa)) return;
+        if (U_split < U1p && !emit_runs(U_split * (R / blkf), U1p * (R / blkf), blkf, Lf, Jf, modef, nbf, faf))
+            return;
         if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
     }
     flush_generic();

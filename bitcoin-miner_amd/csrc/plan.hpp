@@ -88,6 +88,10 @@ struct PlanOpts {
     // with the same code object: +0.6% to +1.9% on configs[1], configs[2]'s halves and the d = 10
     // bucket (profiles/r03u_*).  0: one workgroup per chunk.
     int queue = 1;
+    // Innermost digit (execution of the plan's fast pieces): 1 = where a nonce costs
+    // less with the digit ending the word before the last digit's enumerated innermost (the
+    // kMode*Early layouts, layout.hpp), take that layout; 0 = always the last digit.
+    int early = 1;
     // Round 4 A/B-rejected three more execution knobs and they were removed from the library in
     // round 5 (HISTORY.md §3): full-L pieces below 2^31 / 2^33 nonces on the low-priority stream
     // (-4% / -5%), a finest tail at L - 2 on a third stream (+-0.3%), and the tail split fused

@@ -25,7 +25,7 @@ MH_ENOTREQ = -6
 MH_EINTERNAL = -7
 MH_EREJECTED = -8
 OPS_PER_BLOCK = 1376  # MH_OPS_PER_BLOCK
-MH_ABI_VERSION = 4    # include/minehip.h: the struct layouts below are this version's
+MH_ABI_VERSION = 5    # include/minehip.h: the struct layouts below are this version's
 MH_MAX_WORKERS = 256  # most devices one mh_search_multi / mh_multi_plan call may list
 
 #: every symbol include/*.h declares

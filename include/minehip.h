@@ -56,7 +56,7 @@ extern "C" {
 #define MH_MAX_MSG_LEN (1u << 20)
 
 /* ABI version of this header, returned by mh_abi_version(). */
-#define MH_ABI_VERSION 4
+#define MH_ABI_VERSION 5
 
 int mh_abi_version(void);
 
@@ -183,8 +183,11 @@ typedef struct mh_piece {
     int32_t kind;       /* 0 = fast run kernel, 1 = generic per-nonce kernel */
     int32_t digits;     /* decimal digits of every nonce in the piece */
     int32_t lo_digits;  /* fast: digits enumerated inside a run (L)        */
-    int32_t word;       /* fast: message word holding the last digit (J)   */
-    int32_t mode;       /* fast: 0 one block, 1 prefix block per run, 2 two blocks per nonce */
+    int32_t word;       /* fast: message word of the per-nonce digit (J): the last digit's, or
+                           (modes 3..5) the word before it, whose last byte is then the digit
+                           enumerated innermost (ABI 5) */
+    int32_t mode;       /* fast: 0 one block, 1 prefix block per run, 2 two blocks per nonce;
+                           3, 4, 5 the same with the innermost digit in word J (ABI 5) */
     int32_t blocks;     /* tail blocks hashed per nonce in the final message */
     uint32_t nonce_ops; /* fast: algorithmic VALU instructions per nonce */
     uint32_t nonce_slots; /* fast: the same work in SIMD-32 issue slots */

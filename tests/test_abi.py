@@ -48,7 +48,7 @@ def test_product_library_has_no_dev_hooks():
 def test_abi_version_and_devices():
     hdr = open(os.path.join(ROOT, "include", "minehip.h")).read()
     v = int(re.search(r"#define MH_ABI_VERSION (\d+)", hdr).group(1))
-    assert minehip.lib.mh_abi_version() == v == _lib.MH_ABI_VERSION == 4
+    assert minehip.lib.mh_abi_version() == v == _lib.MH_ABI_VERSION == 5
     assert minehip.device_count() >= 0
 
 
@@ -124,12 +124,20 @@ def check_plan(msg, lo, hi):
             assert p["first"] % R == 0 and p["count"] % R == 0  # whole runs only
             pl = t + d - 1
             base = 64 if (p["blocks"] == 2 and pl >= 64) else 0
-            assert p["word"] == (pl - base) >> 2
-            assert ((pl - base - L + 1) >> 2) >= p["word"] - 1
-            if p["mode"] == 1:
+            mode = p["mode"] % 3
+            if p["mode"] < 3:
+                assert p["word"] == (pl - base) >> 2
+                assert ((pl - base - L + 1) >> 2) >= p["word"] - 1
+            else:  # Early: the innermost digit ends word J, the word before the last digit's
+                assert p["word"] == ((pl - base) >> 2) - 1
+                pos = pl - (base + 4 * p["word"] + 3)  # its decimal position
+                assert 1 <= pos < d
+                block = 10 ** max(L, pos + 1)
+                assert p["first"] % block == 0 and p["count"] % block == 0  # whole blocks of lanes
+            if mode == 1:
                 assert pl - L + 1 >= 64
-            if p["mode"] == 2:
-                assert pl < 64 and 13 <= p["word"] <= 15
+            if mode == 2:
+                assert pl < 64 and 13 <= p["word"] + (p["mode"] >= 3) <= 15
         cur = last + 1
     assert cur - 1 == hi
     return pieces
@@ -162,6 +170,28 @@ def test_plan_fine_tail_covers_exactly(monkeypatch):
         assert tails and all(p["count"] <= 1 << 28 for p in tails)
         check_plan(m, 549755813888, 549755813888 + 6871947673)
         check_plan(m, U64 - (1 << 33), U64)
+
+
+def test_plan_early_layouts_tile_and_cost_less(monkeypatch):
+    """MINEHIP_EARLY (default 1): where the last digit sits in word 1, 9 or 14, a bucket's fast
+    pieces enumerate the digit ending the word before it innermost (fast_search<J, 3..5>); the
+    lanes of one block then interleave (innermost digit at decimal position p >= L), pieces are
+    whole blocks, and the plan still tiles the range exactly -- at a lower algorithmic cost than
+    the last-digit plan of the same range."""
+    cases = ((b"x" * 60, 0, 2 ** 34 - 1, {(0, 4)}),                       # configs[2], two tail blocks
+             ((b"cmu440-" * 10)[:30], 0, 2 ** 32 - 1, {(8, 3)}),          # <9, One> -> <8, OneEarly>
+             ((b"cmu440-" * 10)[:48], 0, 2 ** 32 - 1, {(13, 5)}),         # <14, Two> -> <13, TwoEarly>
+             (b"", 10 ** 6, 10 ** 7 - 1, {(0, 3)}))                        # d = 7: last digit in word 1
+    for m, lo, hi, early in cases:
+        cost = {}
+        for e in (1, 0):
+            monkeypatch.setenv("MINEHIP_EARLY", str(e))
+            pieces = check_plan(m, lo, hi)
+            modes = {(p["word"], p["mode"]) for p in pieces if p["kind"] == 0}
+            assert (modes >= early) if e else not any(md >= 3 for _, md in modes), (m[:8], e, modes)
+            cost[e] = sum(p["count"] * p["nonce_ops"] for p in pieces if p["kind"] == 0)
+            check_plan(m, U64 - (1 << 33), U64)
+        assert cost[1] < cost[0] * 0.995, (m[:8], cost)
 
 
 def test_plan_uses_fast_kernel_for_bulk():
@@ -262,34 +292,44 @@ def test_miner_handle_rejects_non_requests():
     assert e.value.code == minehip.MH_ERANGE
 
 
-KERNELS = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(13, 2), (14, 2), (15, 2)}
+# fast_search<J, MODE>: One J = 0..13, Pre J = 0..4, Two J = 13..15, and the Early modes (the digit
+# ending word J innermost) OneEarly J = 0, 8, PreEarly J = 0, TwoEarly J = 13
+KERNELS = ({(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(13, 2), (14, 2), (15, 2)} |
+           {(0, 3), (8, 3), (0, 4), (13, 5)})
+
+
+KERNEL_CASE_NONCES = 250_000
 
 
 def kernel_cases():
-    """One (msg, lo, hi) per instantiated fast kernel (word J, mode), planned
-    with MINEHIP_GENERIC_BELOW=0 (small buckets on the fast kernels)."""
+    """One (msg, lo, hi, early) per instantiated fast kernel (word J, mode), planned with
+    MINEHIP_GENERIC_BELOW=0 (small buckets on the fast kernels) and MINEHIP_EARLY=early: the
+    default (1) reaches the Early kernels, 0 the last-digit kernels they replace."""
     seen = {}
-    old = os.environ.get("MINEHIP_GENERIC_BELOW")
+    old = {k: os.environ.get(k) for k in ("MINEHIP_GENERIC_BELOW", "MINEHIP_EARLY")}
     os.environ["MINEHIP_GENERIC_BELOW"] = "0"
     try:
-        _kernel_cases(seen)
+        for early in (1, 0):
+            os.environ["MINEHIP_EARLY"] = str(early)
+            _kernel_cases(seen, early)
     finally:
-        if old is None:
-            os.environ.pop("MINEHIP_GENERIC_BELOW")
-        else:
-            os.environ["MINEHIP_GENERIC_BELOW"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return seen
 
 
-def _kernel_cases(seen):
+def _kernel_cases(seen, early):
     for L in range(0, 128):
         m = b"q" * L
         for d in range(2, 21):
             lo = 10 ** (d - 1)
-            hi = min(U64, lo + 5000)
+            hi = min(U64, lo + KERNEL_CASE_NONCES)  # two blocks of an Early layout's lanes (<= 10^5 each)
             for p in minehip.plan(m, lo, hi):
                 if p["kind"] == 0:
-                    seen.setdefault((p["word"], p["mode"]), (m, lo, hi))
+                    seen.setdefault((p["word"], p["mode"]), (m, lo, hi, early))
 
 
 def test_every_instantiated_kernel_is_reachable():
@@ -305,8 +345,8 @@ def test_embedded_code_object_carries_queue_marker():
     assert b"mh_fast_queue_args" in co
     md = codeobj.metadata(co)
     fast = [k for k in md["amdhsa.kernels"] if "fast_search" in k[".name"]]
-    assert len(fast) == 22
-    assert {k[".args"][0][".size"] for k in fast} == {472}      # FastArgs, by value
+    assert len(fast) == len(KERNELS)
+    assert {k[".args"][0][".size"] for k in fast} == {504}      # FastArgs, by value
     nomarker = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
     if os.path.exists(nomarker):
         assert b"mh_fast_queue_args" not in open(nomarker, "rb").read()

@@ -97,17 +97,42 @@ def test_config3_fixture():
                 assert c == (h, n)
 
 
+# the last-digit layouts an Early layout replaces in the default plan of every bucket holding two
+# blocks of its lanes (<= 2 x 10^5 nonces); MINEHIP_EARLY=0 plans them instead
+REPLACED_BY_EARLY = {(1, 0), (1, 1), (9, 0), (14, 2)}
+EARLY_FIXTURES = ("cfg3b", "two14", "two15", "pre2", "one1", "one10")
+
+
+def _used(names, early):
+    import minehip
+    old = os.environ.get("MINEHIP_EARLY")
+    os.environ["MINEHIP_EARLY"] = str(early)
+    try:
+        used = set()
+        for name in names:
+            msg, lo, hi = _cfg(name)
+            used |= {(p["word"], p["mode"]) for p in minehip.plan(msg, lo, hi) if p["kind"] == 0}
+        if early:
+            for lo, hi, _, _ in load_golden("fullsize_cfg4s.json")["samples"]:
+                used |= {(p["word"], p["mode"]) for p in minehip.plan(b"cmu440", lo, hi) if p["kind"] == 0}
+        return used
+    finally:
+        if old is None:
+            os.environ.pop("MINEHIP_EARLY")
+        else:
+            os.environ["MINEHIP_EARLY"] = old
+
+
 def test_fixtures_cover_every_fast_layout():
     """The default plans of the full-size fixtures' ranges (host-only mh_plan) use every
-    fast_search<J, MODE> instantiation the default plan can ever choose: all 22 but <0, One>,
-    whose last digit would sit in message bytes 0..3, i.e. d <= 4 -- always a bucket of fewer
-    than 2^20 nonces, which goes to the generic kernel."""
-    import minehip
-    used = set()
-    for name in CFGS:
-        msg, lo, hi = _cfg(name)
-        used |= {(p["word"], p["mode"]) for p in minehip.plan(msg, lo, hi) if p["kind"] == 0}
-    for lo, hi, _, _ in load_golden("fullsize_cfg4s.json")["samples"]:
-        used |= {(p["word"], p["mode"]) for p in minehip.plan(b"cmu440", lo, hi) if p["kind"] == 0}
-    every = {(j, 0) for j in range(14)} | {(j, 1) for j in range(5)} | {(j, 2) for j in (13, 14, 15)}
-    assert used == every - {(0, 0)}, sorted(every - used)
+    fast_search<J, MODE> instantiation the default plan chooses for a bucket of more than two
+    Early blocks: all 26 but <0, One>, whose last digit would sit in message bytes 0..3, i.e.
+    d <= 4 -- always a bucket of fewer than 2^20 nonces, which goes to the generic kernel --
+    and the four last-digit layouts the Early ones replace.  Those four are what
+    the same fixtures plan with MINEHIP_EARLY=0 (tests/test_gpu_fullsize.py runs both)."""
+    from test_abi import KERNELS
+    used = _used(CFGS, 1)
+    assert used == KERNELS - {(0, 0)} - REPLACED_BY_EARLY, sorted(KERNELS - used)
+    assert _used(EARLY_FIXTURES, 0) >= REPLACED_BY_EARLY
+    for name in EARLY_FIXTURES:  # exactly these fixtures change kernels with the knob
+        assert _used((name,), 1) != _used((name,), 0), name

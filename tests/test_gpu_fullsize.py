@@ -17,7 +17,10 @@ reproduce every one of them:
   one1, one5, one7, one8, one10, one12
          ("cmu440-" repeated)[:n], n = 0/13/21/25/30/41, [0, 2^32-1]: one tail block,
          d = 7..10 in <1|2|5|7|8|9|10|12, One>; with the rest every layout the
-         default plan uses (test_fullsize_fixtures.py checks the coverage)
+         default plan uses (test_fullsize_fixtures.py checks the coverage).  Where a
+         bucket's default layout is an Early one (<0|8, OneEarly>, <0, PreEarly>,
+         <13, TwoEarly>: cfg3b, two14, two15, pre2, one1, one10) the named last-digit
+         kernel runs with MINEHIP_EARLY=0, and both are checked
   pre3, pre4, top
          2^32 nonces from 10^13 and 10^17 for the 62-byte message (<3, Pre>, <4, Pre>),
          and "cmu440" over [2^64-2^32, 2^64-1] (20 digits, <6, One>, up to the last u64)
@@ -67,6 +70,23 @@ def test_every_chunk(gpu, name):
 def test_whole_range(gpu, name):
     msg, lo, hi, _, result, _ = fixture(name)
     assert gpu.search(msg, lo, hi) == result
+
+
+# the fixtures whose default plan takes an Early layout (the digit ending the word before the last
+# digit's innermost, fast_search<J, 3..5>): the same chunks and whole range with MINEHIP_EARLY=0,
+# on the last-digit kernels the Early ones replace, so both orders are pinned at full size
+EARLY = ("cfg3b", "two14", "two15", "pre2", "one1", "one10")
+
+
+@pytest.mark.parametrize("name", EARLY)
+def test_every_chunk_last_digit_innermost(gpu, name):
+    msg, lo, hi, bits, result, chunks = fixture(name)
+    size = 1 << bits
+    with env(MINEHIP_EARLY=0):
+        bad = [(i, exp) for i, exp in enumerate(chunks)
+               if gpu.search(msg, lo + i * size, min(hi, lo + (i + 1) * size - 1)) != exp]
+        assert not bad, f"{len(bad)} of {len(chunks)} chunks differ, first: {bad[:3]}"
+        assert gpu.search(msg, lo, hi) == result
 
 
 def test_config2_and_shards(gpu):

@@ -109,17 +109,18 @@ def test_every_tail_offset_and_bucket(gpu):
 
 
 def test_every_kernel_instantiation(gpu):
-    """Each of the 22 fast_search<J, MODE> kernels, at the shortest and the
+    """Each of the 26 fast_search<J, MODE> kernels, at the shortest and the
     longest lane runs (L = 1 and the largest L the layout allows), bit-exact
-    against the oracle over ranges holding whole runs plus ragged edges."""
-    from test_abi import KERNELS, kernel_cases
+    against the oracle over ranges holding whole runs (an Early layout: whole
+    blocks of interleaved lanes) plus ragged edges."""
+    from test_abi import KERNELS, KERNEL_CASE_NONCES, kernel_cases
     cases = kernel_cases()
     assert set(cases) == KERNELS
-    for (J, mode), (m, lo, _) in sorted(cases.items()):
-        hi = lo + 23_456
+    for (J, mode), (m, lo, _, early) in sorted(cases.items()):
+        hi = lo + KERNEL_CASE_NONCES + 3_456
         exp = oracle.search(m, lo, hi, threads=8)
         for Ld in (1, 3):
-            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
+            with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0, MINEHIP_EARLY=early):
                 assert gpu.search(m, lo, hi) == exp, (J, mode, len(m), Ld)
 
 

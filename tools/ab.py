@@ -38,6 +38,10 @@ WORKLOADS = {
     "shard4": ("cmu440", 1 << 39, 13743895347),           # one 4-GPU shard
     "shard2": ("cmu440", 1 << 39, 27487790694),           # one 2-GPU shard
     "p55": (("cmu440-" * 10)[:55], 0, 1 << 32),           # <13|14|15, Two> layouts
+    # round 5: fixtures whose d = 10 bucket takes an Early layout (fast_search<J, 3..5>)
+    "one10": (("cmu440-" * 10)[:30], 0, 1 << 32),         # <9, One> -> <8, OneEarly>
+    "two14": (("cmu440-" * 10)[:48], 0, 1 << 32),         # <14, Two> -> <13, TwoEarly>
+    "pre2": (("cmu440-" * 10)[:62], 0, 1 << 32),          # d = 9: <1, Pre> -> <0, PreEarly>
 }
 FATAL = {124, 134, 137, 139}
 
