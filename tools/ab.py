@@ -42,6 +42,11 @@ WORKLOADS = {
     "one10": (("cmu440-" * 10)[:30], 0, 1 << 32),         # <9, One> -> <8, OneEarly>
     "two14": (("cmu440-" * 10)[:48], 0, 1 << 32),         # <14, Two> -> <13, TwoEarly>
     "pre2": (("cmu440-" * 10)[:62], 0, 1 << 32),          # d = 9: <1, Pre> -> <0, PreEarly>
+    # ... and one bucket of each, alone
+    "x60d10": ("x" * 60, 10 ** 9, 1 << 33),               # <1, Pre> -> <0, PreEarly>, p = 3
+    "x60d11": ("x" * 60, 10 ** 10, 1 << 33),              # <1, Pre> -> <0, PreEarly>, p = 4
+    "one10d9": (("cmu440-" * 10)[:30], 10 ** 8, 9 * 10 ** 8),   # <9, One> -> <8, OneEarly>
+    "two14d10": (("cmu440-" * 10)[:48], 10 ** 9, 1 << 32),      # <14, Two> -> <13, TwoEarly>
 }
 FATAL = {124, 134, 137, 139}
 
