@@ -194,6 +194,19 @@ def test_plan_early_layouts_tile_and_cost_less(monkeypatch):
         assert cost[1] < cost[0] * 0.995, (m[:8], cost)
 
 
+def test_plan_early_every_position_tiles():
+    """The ranges test_gpu_parity.py::test_early_layout_every_position runs on the GPU (every
+    Early kernel x innermost position p = 1..4 x L = 1..3, the u64 top included) are planned as
+    exact tilings of whole blocks."""
+    from test_gpu_parity import early_position_cases, env
+    cases = early_position_cases()
+    assert {(k[0], k[1], k[2]) for k in cases} >= {(j, m, p) for j, m in ((8, 3), (0, 4), (13, 5))
+                                                     for p in (1, 2, 3, 4)}
+    for (m, lo, hi, Ld) in cases.values():
+        with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
+            check_plan(m, lo, hi)
+
+
 def test_plan_uses_fast_kernel_for_bulk():
     pieces = check_plan(b"cmu440", 0, 2 ** 32 - 1)
     fast = sum(p["count"] for p in pieces if p["kind"] == 0)

@@ -124,6 +124,50 @@ def test_every_kernel_instantiation(gpu):
                 assert gpu.search(m, lo, hi) == exp, (J, mode, len(m), Ld)
 
 
+def early_position_cases(Ls=(1, 2, 3)):
+    """(msg, lo, hi, L, J, mode, p) for every (Early kernel, innermost position p, L) the planner
+    can produce: messages of every tail offset, each bucket d = 2..20 from its first nonce (and
+    the top of the u64 range for d = 20), two blocks of lanes plus a ragged edge.  Host only."""
+    import minehip
+    cases = {}
+    for n in range(0, 128):
+        m = b"q" * n
+        t = (n + 1) % 64
+        for d in range(2, 21):
+            for Ld in Ls:
+                with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
+                    los = [10 ** (d - 1)] + ([U64 - 250_000] if d == 20 else [])
+                    for lo in los:
+                        hi = min(U64, lo + 2 * 10 ** 5 + 3_456)
+                        for pc in minehip.plan(m, lo, hi):
+                            if pc["kind"] != 0 or pc["mode"] < 3:
+                                continue
+                            pl = t + pc["digits"] - 1
+                            base = 64 if (pc["blocks"] == 2 and pl >= 64) else 0
+                            pos = pl - (base + 4 * pc["word"] + 3)
+                            assert 1 <= pos <= 4, (n, lo, pc)
+                            key = (pc["word"], pc["mode"], pos, pc["lo_digits"], lo == los[-1] and d == 20)
+                            cases.setdefault(key, (m, lo, hi, Ld))
+    return cases
+
+
+def test_early_layout_every_position(gpu):
+    """Each Early kernel (the digit ending word J innermost) at every decimal position p of that
+    digit and every lane length L it is planned with -- contiguous lanes (p < L, the group digits
+    around p) and interleaved ones (p >= L, U's digits around p) -- and at the top of the u64
+    range: bit-exact against the oracle, and against the last-digit plan (MINEHIP_EARLY=0)."""
+    cases = early_position_cases()
+    kinds = {(J, mode) for (J, mode, *_rest) in cases}
+    assert kinds == {(0, 3), (8, 3), (0, 4), (13, 5)}, kinds
+    assert any(p < L for (_, _, p, L, _) in cases) and any(p >= L for (_, _, p, L, _) in cases)
+    for key, (m, lo, hi, Ld) in sorted(cases.items()):
+        exp = oracle.search(m, lo, hi, threads=8)
+        with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
+            assert gpu.search(m, lo, hi) == exp, (key, len(m), lo, hi)
+            with env(MINEHIP_EARLY=0):
+                assert gpu.search(m, lo, hi) == exp, (key, "last digit")
+
+
 def test_u64_edges(gpu):
     for m in (b"cmu440", b"", b"q" * 60, b"r" * 119):
         top = oracle.search(m, U64 - 30000, U64, threads=8)

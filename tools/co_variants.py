@@ -6,6 +6,8 @@ build's MINEHIP_DEV_CODE_OBJECT hook (round 3):
          lines (the loop header is not aligned by the compiler)
   cmpH   the per-nonce loop's v_cmp_ge_u32_e32 classed half rate (measured:
          v_cmp_lt_u32_e32 issues at 62 lanes/clk/CU, profiles/r03b_valu_ops.json)
+  earlyW the product build (add3 split + issue-priority pass) with the Early kernels compiled
+         for W waves per SIMD (-DMH_EARLY_WAVES=W; round 5)
 
   python tools/co_variants.py pad0 pad1 pad4 cmpH   # -> build/ab/<variant>.hsaco
 """
@@ -44,6 +46,13 @@ def main():
         if v.startswith("pad"):
             text, _ = issue_prio.annotate(src)
             text = pad(text, int(v[3:]))
+        elif v.startswith("early"):
+            import add3_split
+            s = os.path.join(ROOT, "build", "ab", v + "_src.s")
+            subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                            f"-DMH_EARLY_WAVES={int(v[5:])}", "--cuda-device-only", "-S", "-o", s,
+                            os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "fast_search.hip")], check=True)
+            text, _ = issue_prio.annotate(add3_split.split(open(s).read(), 3)[0])
         elif v == "cmpH":
             cmps = {o for o in valu_rates.FULL if o.startswith("v_cmp_")}
             old = valu_rates.FULL, valu_rates.HALF
