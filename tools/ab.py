@@ -19,6 +19,7 @@ The recipes under tools/ab/ are the experiments behind DESIGN.md and profiles/ (
 import argparse
 import json
 import os
+import re
 import subprocess
 import sys
 
@@ -59,6 +60,12 @@ def load(path):
         variants[name] = f"MINEHIP_DEV_CODE_OBJECT={co}"
     if not variants or not r.get("workloads"):
         raise SystemExit(f"{path}: a recipe needs variants and workloads")
+    # kbench.py reads a variant as comma-separated K=V settings; anything else would reach the
+    # library as part of one value (round 5 found r04_fuse_tail's "A=1 B=2" variants set only A)
+    for name, env in variants.items():
+        for kv in filter(None, env.split(",")):
+            if not re.fullmatch(r"MINEHIP_\w+=[^\s=]*", kv) and not r.get("retired"):
+                raise SystemExit(f"{path}: variant {name!r}: {kv!r} is not one MINEHIP_*=value setting")
     for w in r["workloads"]:
         if w[0] not in WORKLOADS:
             raise SystemExit(f"{path}: unknown workload {w[0]!r} (known: {', '.join(WORKLOADS)})")
