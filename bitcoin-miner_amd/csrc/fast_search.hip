@@ -27,15 +27,18 @@
 // occupancy the layout reaches as a one-chunk-per-workgroup kernel (VGPRs 59..79 -> 7 or 6 waves,
 // the Two layouts 98..110 -> 4).  The work-queue loop around the chunk body would otherwise let
 // the allocator take 4..6 more VGPRs and cost a wave per SIMD.  -DMH_MIN_WAVES=n overrides all.
-// The Early modes (layout.hpp) take the occupancy of their tail layout, or MH_EARLY_WAVES.
+// The Early modes (layout.hpp) of the one-block and Pre layouts take 7 (72 VGPRs, spills outside
+// the per-nonce loop only): against their layouts' 6, +0.1% to +1.1% on the three buckets of the
+// round-5 A/B (profiles/r05d_kbench_early_waves_*.json); TwoEarly keeps Two's 4 (at 6 or 7 it
+// spills 56-120 B).  -DMH_EARLY_WAVES=n overrides the One/Pre Early kernels' budget.
 #ifndef MH_EARLY_WAVES
-#define MH_EARLY_WAVES 0
+#define MH_EARLY_WAVES 7
 #endif
 constexpr int min_waves(int J, int MODE) {
 #ifdef MH_MIN_WAVES
     return MH_MIN_WAVES;
 #else
-    return (MODE >= 3 && MH_EARLY_WAVES) ? MH_EARLY_WAVES
+    return (MODE == 3 || MODE == 4) ? MH_EARLY_WAVES
          : MODE % 3 == 2 ? 4
          : MODE % 3 == 1 ? ((J == 0 || J == 4) ? 6 : 7)
                          : ((J == 7 || J == 8 || J >= 10) ? 6 : 7);

@@ -115,8 +115,9 @@ def test_resources_from_the_embedded_code_object():
     mix = bench.fast_loop_mix()
     for k, r in res.items():
         # the work-queue loop around the chunk body leaves a few bytes of spill in some layouts'
-        # per-chunk setup (fast_search.hip min_waves), never inside the per-nonce loop
-        assert r["scratch_bytes"] <= 32 and mix[k]["loop_spill_ops"] == 0, (k, r["scratch_bytes"])
+        # per-chunk setup (fast_search.hip min_waves; <8, OneEarly> at 7 waves: 48 B), never
+        # inside the per-nonce loop
+        assert r["scratch_bytes"] <= 48 and mix[k]["loop_spill_ops"] == 0, (k, r["scratch_bytes"])
         assert 32 <= r["vgpr"] <= 128 and r["agpr"] == 0, k
         assert r["max_waves_per_simd"] >= 4, k
     p = dominant_piece("2")

@@ -6,8 +6,8 @@ build's MINEHIP_DEV_CODE_OBJECT hook (round 3):
          lines (the loop header is not aligned by the compiler)
   cmpH   the per-nonce loop's v_cmp_ge_u32_e32 classed half rate (measured:
          v_cmp_lt_u32_e32 issues at 62 lanes/clk/CU, profiles/r03b_valu_ops.json)
-  earlyW the product build (add3 split + issue-priority pass) with the Early kernels compiled
-         for W waves per SIMD (-DMH_EARLY_WAVES=W; round 5)
+  earlyW the product build (add3 split + issue-priority pass) with the One/Pre Early kernels
+         compiled for W waves per SIMD (-DMH_EARLY_WAVES=W; round 5)
 
   python tools/co_variants.py pad0 pad1 pad4 cmpH   # -> build/ab/<variant>.hsaco
 """

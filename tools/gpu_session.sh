@@ -198,6 +198,15 @@ for s in $STEPS; do
           --no-clock > "$OUT/dist8_cfg4.json" 2> "$OUT/dist8_cfg4.err"
       rc=$?; echo "dist8 cfg4 rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/dist8_cfg4.json"; fatal $rc
       ;;
+    earlypmc)
+      # round 5: configs[2]'s 60 x 'x' line with the Early layout (default) and without, PMC passes
+      # included: VALU per nonce, issue per quad-cycle and waves per SIMD of each dominant kernel
+      for e in 1 0; do
+        MINEHIP_EARLY=$e timeout -k 10 600 python "$ROOT/bench.py" --config 3b --steps 5 --warmup 2 --no-cpu-baseline \
+            > "$OUT/bench_cfg3b_early$e.json" 2> "$OUT/bench_cfg3b_early$e.err"
+        rc=$?; echo "earlypmc $e rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
+      done
+      ;;
     ab:*)
       # an A/B recipe (tools/ab.py, tools/ab/<recipe>.json): one kbench process per workload
       recipe=${s#ab:}
