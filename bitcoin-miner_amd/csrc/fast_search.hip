@@ -31,14 +31,19 @@
 // the per-nonce loop only): against their layouts' 6, +0.1% to +1.1% on the three buckets of the
 // round-5 A/B (profiles/r05d_kbench_early_waves_*.json); TwoEarly keeps Two's 4 (at 6 or 7 it
 // spills 56-120 B).  -DMH_EARLY_WAVES=n overrides the One/Pre Early kernels' budget.
+// -DMH_ONEPRE_WAVES=n (A/B builds, tools/co_variants.py) sets every One/Pre kernel's budget.
 #ifndef MH_EARLY_WAVES
 #define MH_EARLY_WAVES 7
+#endif
+#ifndef MH_ONEPRE_WAVES
+#define MH_ONEPRE_WAVES 0
 #endif
 constexpr int min_waves(int J, int MODE) {
 #ifdef MH_MIN_WAVES
     return MH_MIN_WAVES;
 #else
-    return (MODE == 3 || MODE == 4) ? MH_EARLY_WAVES
+    return (MH_ONEPRE_WAVES && MODE % 3 != 2) ? MH_ONEPRE_WAVES
+         : (MODE == 3 || MODE == 4) ? MH_EARLY_WAVES
          : MODE % 3 == 2 ? 4
          : MODE % 3 == 1 ? ((J == 0 || J == 4) ? 6 : 7)
                          : ((J == 7 || J == 8 || J >= 10) ? 6 : 7);

@@ -48,6 +48,9 @@ WORKLOADS = {
     "x60d11": ("x" * 60, 10 ** 10, 1 << 33),              # <1, Pre> -> <0, PreEarly>, p = 4
     "one10d9": (("cmu440-" * 10)[:30], 10 ** 8, 9 * 10 ** 8),   # <9, One> -> <8, OneEarly>
     "two14d10": (("cmu440-" * 10)[:48], 10 ** 9, 1 << 32),      # <14, Two> -> <13, TwoEarly>
+    "a100d10": ("a" * 100, 10 ** 9, 1 << 33),             # configs[2]'s 100 x 'a' d = 10 bucket, <11, One>
+    "one10d10": (("cmu440-" * 10)[:30], 10 ** 9, 1 << 32),      # <10, One>
+    "one8": (("cmu440-" * 10)[:25], 0, 1 << 32),          # <7|8, One>
 }
 FATAL = {124, 134, 137, 139}
 

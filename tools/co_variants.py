@@ -8,6 +8,7 @@ build's MINEHIP_DEV_CODE_OBJECT hook (round 3):
          v_cmp_lt_u32_e32 issues at 62 lanes/clk/CU, profiles/r03b_valu_ops.json)
   earlyW the product build (add3 split + issue-priority pass) with the One/Pre Early kernels
          compiled for W waves per SIMD (-DMH_EARLY_WAVES=W; round 5)
+  onepreW the same with every One/Pre kernel compiled for W waves (-DMH_ONEPRE_WAVES=W)
 
   python tools/co_variants.py pad0 pad1 pad4 cmpH   # -> build/ab/<variant>.hsaco
 """
@@ -46,11 +47,12 @@ def main():
         if v.startswith("pad"):
             text, _ = issue_prio.annotate(src)
             text = pad(text, int(v[3:]))
-        elif v.startswith("early"):
+        elif v.startswith(("early", "onepre")):
             import add3_split
             s = os.path.join(ROOT, "build", "ab", v + "_src.s")
+            macro = "MH_EARLY_WAVES" if v.startswith("early") else "MH_ONEPRE_WAVES"
             subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
-                            f"-DMH_EARLY_WAVES={int(v[5:])}", "--cuda-device-only", "-S", "-o", s,
+                            f"-D{macro}={int(v.lstrip('abcdefghijklmnopqrstuvwxyz'))}", "--cuda-device-only", "-S", "-o", s,
                             os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "fast_search.hip")], check=True)
             text, _ = issue_prio.annotate(add3_split.split(open(s).read(), 3)[0])
         elif v == "cmpH":
