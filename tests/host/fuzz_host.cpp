@@ -65,6 +65,56 @@ static uint64_t interesting_u64() {
     }
 }
 
+// The digits fast_search writes for lane u, group g and innermost digit i of a fast piece (its
+// per-run formatting of U, the group digits and the per-nonce digit, restated from fast_search.hip
+// on the host), read back as a decimal number, must be the nonce its candidate formula reports,
+// inside the piece -- for the last-digit layouts and the Early ones (interleaved lanes included).
+static uint64_t spread(uint64_t x, uint32_t k) {  // fast_search.hip spread()
+    if (k >= 20u) return x;
+    uint64_t lo = 0, q = 1;
+    for (uint32_t j = 0; j < k; ++j) {
+        lo += (x % 10u) * q;
+        q *= 10u;
+        x /= 10u;
+    }
+    return x * q * 10u + lo;
+}
+static uint64_t g_fast_checked = 0, g_early_checked = 0;
+static bool lanes_format_their_nonces(const mh::Prefix& pre, const mh::Piece& p) {
+    const mh::FastArgs& a = p.fa;
+    const bool early = a.mode >= 3;
+    ++g_fast_checked;
+    g_early_checked += early ? 1u : 0u;
+    const uint32_t base = (a.mode % 3 == mh::kModePre) ? 64u : 0u;
+    const uint32_t d = (uint32_t)p.digits;
+    for (int probe = 0; probe < 4; ++probe) {
+        const uint64_t lane = probe == 0 ? 0 : probe == 1 ? a.n_runs - 1u : rnd(a.n_runs);
+        const uint64_t U = a.u_start + lane;
+        const uint32_t g = (uint32_t)rnd(a.n_groups), i = (uint32_t)rnd(10);
+        uint8_t b[128];
+        for (uint32_t x = 0; x < 128; ++x) b[x] = (uint8_t)(a.blk[x >> 2] >> (24u - 8u * (x & 3u)));
+        uint64_t u = U;
+        for (uint32_t k = 0; k < a.n_hi; ++k, u /= 10u)
+            b[a.hi_end - 1u - k - ((early && k >= a.hole) ? 1u : 0u)] += (uint8_t)(u % 10u);
+        uint32_t gq = g;
+        for (uint32_t j = 0; j + 1u < a.L; ++j, gq /= 10u) {
+            const uint32_t pos = early ? a.g_last - j - (j >= a.g_hole ? 1u : 0u) : a.lo_pos + (a.L - 2u - j);
+            b[base + pos] += (uint8_t)(gq % 10u);
+        }
+        b[base + (early ? a.inner : a.lo_pos + a.L - 1u)] += (uint8_t)i;
+        uint64_t n = 0;
+        for (uint32_t x = 0; x < d; ++x) {
+            const uint8_t c = b[pre.t + x];
+            if (c < '0' || c > '9' || (x == 0 && c == '0' && d > 1)) return false;
+            n = n * 10u + (uint64_t)(c - '0');
+        }
+        const uint64_t want = early ? spread(U, a.hole) * a.u_mul + spread(g, a.g_hole) + i * a.i_mul
+                                    : U * a.pow10L + (uint64_t)g * 10u + i;
+        if (n != want || n < p.first || n - p.first >= p.count) return false;
+    }
+    return true;
+}
+
 // planner: pieces tile [lo, hi] in order, in-bounds shapes
 static void fuzz_plan() {
     std::string msg(rnd(700), 'a');
@@ -79,6 +129,8 @@ static void fuzz_plan() {
     o.min_lanes = rnd(2) ? 1 : (1ull << rnd(20));
     o.max_nonces_per_launch = 1ull + rnd(1ull << 33);
     o.generic_below = rnd(2) ? 0 : rnd(1ull << 21);
+    o.early = (int)rnd(2);
+    o.fine_tail = rnd(2) ? 0 : rnd(1ull << 29);
     uint64_t cur = lo;
     bool done = false, bad = false;
     size_t n = 0;
@@ -90,7 +142,8 @@ static void fuzz_plan() {
         if (p.kind == 0) {
             const uint64_t R = kP10[p.L];
             if (p.L < 1 || p.L > 5 || p.first % R || p.count % R || p.fa.n_runs == 0 ||
-                (uint64_t)p.fa.n_runs * R != p.count || p.fa.n_hi + p.fa.L > 20) {
+                (uint64_t)p.fa.n_runs * R != p.count || p.fa.n_hi + p.fa.L > 20 ||
+                !lanes_format_their_nonces(pre, p)) {
                 bad = true;
                 return false;
             }
@@ -264,6 +317,8 @@ int main(int argc, char** argv) {
         if (i % 4 == 0) fuzz_sched();
         if (i % 4 == 0) fuzz_server();
     }
-    printf("fuzz_host seed=%llu iters=%d failures=%d\n", (unsigned long long)seed, iters, g_fail);
+    printf("fuzz_host seed=%llu iters=%d failures=%d fast_pieces=%llu early_pieces=%llu\n",
+           (unsigned long long)seed, iters, g_fail, (unsigned long long)g_fast_checked,
+           (unsigned long long)g_early_checked);
     return g_fail ? 1 : 0;
 }

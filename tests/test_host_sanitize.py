@@ -45,6 +45,11 @@ def test_host_fuzz_under_sanitizers(fuzz_bin, seed):
     r = subprocess.run([fuzz_bin, str(seed), "150"], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "failures=0" in r.stdout
+    # fast pieces whose lanes' formatted digits were checked against the kernel's nonce formula,
+    # Early layouts (interleaved lanes) among them
+    import re
+    m = re.search(r"fast_pieces=(\d+) early_pieces=(\d+)", r.stdout)
+    assert m and int(m.group(1)) > 10000 and int(m.group(2)) > 1000, r.stdout
 
 
 @pytest.fixture(scope="module", params=["address,undefined", "thread"])
