@@ -9,6 +9,8 @@ build's MINEHIP_DEV_CODE_OBJECT hook (round 3):
   earlyW the product build (add3 split + issue-priority pass) with the One/Pre Early kernels
          compiled for W waves per SIMD (-DMH_EARLY_WAVES=W; round 5)
   onepreW the same with every One/Pre kernel compiled for W waves (-DMH_ONEPRE_WAVES=W)
+  thinN  the product build with a priority marker only where the VALU run it starts is at least N
+         instructions long (shorter runs keep the priority they follow): fewer s_setprio per nonce
 
   python tools/co_variants.py pad0 pad1 pad4 cmpH   # -> build/ab/<variant>.hsaco
 """
@@ -39,8 +41,41 @@ def pad(text, n):
                   text, flags=re.M)
 
 
+def thin_annotate(text, min_run):
+    """issue_prio.annotate, but a class change emits its marker only when the run of same-class
+    VALU instructions it starts (within the block) is at least min_run long."""
+    lines = text.split("\n")
+    cls = [issue_prio.valu_class(l) for l in lines]
+    out, n, cur, in_kernel = [], 0, None, False
+    for k, line in enumerate(lines):
+        if re.match(r"^_Z\S+:", line):
+            in_kernel, cur = True, None
+        elif line.startswith(".Lfunc_end"):
+            in_kernel = False
+        elif re.match(r"^\.LBB\w*:", line):
+            cur = None
+        c = cls[k]
+        if in_kernel and c is not None and c != cur:
+            run = 0
+            for j in range(k, len(lines)):
+                if re.match(r"^\.LBB\w*:", lines[j]) and j > k:
+                    break
+                if cls[j] is None:
+                    continue
+                if cls[j] != c:
+                    break
+                run += 1
+            if cur is None or run >= min_run:
+                out.append(f"\ts_setprio {issue_prio.PRIO_HALF if c == 'H' else issue_prio.PRIO_FULL}")
+                n += 1
+                cur = c
+        out.append(line)
+    return "\n".join(out), n
+
+
 def main():
     src = open(os.path.join(ROOT, "build", "fast_search.s")).read()
+    src_prod = src
     os.makedirs(os.path.join(ROOT, "build", "ab"), exist_ok=True)
     for v in sys.argv[1:]:
         out = os.path.join(ROOT, "build", "ab", v + ".hsaco")
@@ -55,6 +90,9 @@ def main():
                             f"-D{macro}={int(v.lstrip('abcdefghijklmnopqrstuvwxyz'))}", "--cuda-device-only", "-S", "-o", s,
                             os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "fast_search.hip")], check=True)
             text, _ = issue_prio.annotate(add3_split.split(open(s).read(), 3)[0])
+        elif v.startswith("thin"):
+            import add3_split
+            text, _ = thin_annotate(add3_split.split(src_prod, 3)[0], int(v[4:]))
         elif v == "cmpH":
             cmps = {o for o in valu_rates.FULL if o.startswith("v_cmp_")}
             old = valu_rates.FULL, valu_rates.HALF
