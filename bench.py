@@ -959,9 +959,14 @@ def main():
     my_lo, my_hi = (rank_range(cfg, rank, world, 0, steps) if launched else (job_lo, job_hi))
     pieces = []
     for var in kst[:2]:
+        # the PMC passes tell launches apart by kernel name only: a second variant that is the same
+        # kernel at another lane length (e.g. a bucket's tail split) gets no PMC pass of its own
+        if pieces and (var["word"], var["mode"]) == (pieces[0]["word"], pieces[0]["mode"]):
+            break
         p = largest_piece(msg, my_lo, my_hi, var)
-        if p is not None:
-            pieces.append(p)
+        if p is None:
+            break
+        pieces.append(p)
     if pieces:
         p = pieces[0]
         roof["algorithmic_bytes_per_launch"] = -(-(p["count"] // 10 ** p["lo_digits"]) // 256) * 16
