@@ -99,7 +99,7 @@ def test_balanced_strong_shards_follow_rates():
     and the merged result is the full scan's."""
     world, bits, steps = 2, 16, 4
     cfg = dict(msg="cmu440", bits=bits, scaling="strong")
-    out = _launch(world, cfg, steps, balance=True, slow_ns=2000, warmup=3)
+    out = _launch(world, cfg, steps, balance=True, slow_ns=10000, warmup=3)  # sleeps >> scheduling noise
     lo, hi = 0, (1 << bits) - 1
     assert all(o[1] == oracle.search(MSG, lo, hi) for o in out)
     assert _tiles_once(out, lo, hi)
