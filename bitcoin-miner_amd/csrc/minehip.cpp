@@ -83,13 +83,9 @@ struct DevCtx {
     int dev = -1;
     bool ready = false;
     hipStream_t stream = nullptr;              // every search's merge and copy; pieces with streams = 1
-    // streams = 2: the pieces' streams, by priority: [0] coarse pieces (high), [1] the other pieces
-    // (low); streams = 3 (experiment): [2] a second high-priority stream, the coarse pieces
-    // alternating between [0] and [2] so that consecutive coarse launches run side by side
-    hipStream_t ps[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t ev_piece[3] = {nullptr, nullptr, nullptr};  // each piece stream's work so far
-    int nps = 2;       // piece streams this search uses
-    int coarse_k = 0;  // coarse pieces enqueued by this search
+    // streams = 2: the pieces' streams, by priority: [0] coarse pieces (high), [1] the other pieces (low)
+    hipStream_t ps[2] = {nullptr, nullptr};
+    hipEvent_t ev_piece[2] = {nullptr, nullptr};  // each piece stream's work so far
     hipEvent_t ev_main = nullptr;                          // the main stream's (reset / merge)
     Partial* d_partials = nullptr;
     Partial* d_best = nullptr;
@@ -143,12 +139,11 @@ int init_locked(DevCtx* c, int dev) {
     // each resource only once: a call after a failed init (e.g. the code object
     // did not load) resumes where that one stopped instead of allocating again
     if (!c->stream) MH_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    if (!c->ps[0] || !c->ps[1] || !c->ps[2]) {
+    if (!c->ps[0] || !c->ps[1]) {
         int least = 0, greatest = 0;
         MH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));  // gfx950: 1 .. -1
         if (!c->ps[0]) MH_HIP(hipStreamCreateWithPriority(&c->ps[0], hipStreamNonBlocking, greatest));
         if (!c->ps[1]) MH_HIP(hipStreamCreateWithPriority(&c->ps[1], hipStreamNonBlocking, least));
-        if (!c->ps[2]) MH_HIP(hipStreamCreateWithPriority(&c->ps[2], hipStreamNonBlocking, greatest));
     }
     for (auto& e : c->ev_piece)
         if (!e) MH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -186,7 +181,7 @@ int harvest_locked(DevCtx* c) {
 // The piece streams start after the main stream's work so far (the reset, a merge).
 int piece_streams_wait_main(DevCtx* c) {
     MH_HIP(hipEventRecord(c->ev_main, c->stream));
-    for (int k = 0; k < c->nps; ++k) MH_HIP(hipStreamWaitEvent(c->ps[k], c->ev_main, 0));
+    for (auto s : c->ps) MH_HIP(hipStreamWaitEvent(s, c->ev_main, 0));
     return MH_OK;
 }
 
@@ -196,7 +191,7 @@ int piece_streams_wait_main(DevCtx* c) {
 int flush_partials(DevCtx* c, bool split) {
     if (!c->poff) return MH_OK;
     if (split) {
-        for (int k = 0; k < c->nps; ++k) {
+        for (int k = 0; k < 2; ++k) {
             MH_HIP(hipEventRecord(c->ev_piece[k], c->ps[k]));
             MH_HIP(hipStreamWaitEvent(c->stream, c->ev_piece[k], 0));
         }
@@ -215,8 +210,7 @@ bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) { return p.kind =
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
 int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool split) {
-    hipStream_t s = c->stream;
-    if (split) s = !coarse_piece(p, opt) ? c->ps[1] : c->ps[(c->nps == 3 && (c->coarse_k++ & 1)) ? 2 : 0];
+    hipStream_t s = !split ? c->stream : c->ps[coarse_piece(p, opt) ? 0 : 1];
     uint32_t blocks;
     if (p.kind == 0) {
         // host-side shape checks: the grid covers exactly n_runs lanes and the
@@ -245,7 +239,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
     if (c->prof) {
         if (c->used == kEventPairs) {
             MH_HIP(hipStreamSynchronize(c->stream));
-            for (int k = 0; k < c->nps; ++k) MH_HIP(hipStreamSynchronize(c->ps[k]));
+            for (auto ps : c->ps) MH_HIP(hipStreamSynchronize(ps));
             int rc = harvest_locked(c);
             if (rc) return rc;
         }
@@ -287,8 +281,7 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
 //   MINEHIP_GENERIC_BELOW  buckets with fewer nonces go to the generic kernel (2^20)
 //   MINEHIP_MAX_BLOCKS     workgroups per launch (1..kMaxBlocksPerLaunch)
 //   MINEHIP_STREAMS        1: one stream; 2: coarse / fine pieces on high / low priority
-//                          streams (default 2); 3 (experiment): the coarse pieces alternate
-//                          between two high-priority streams
+//                          streams (default 2)
 //   MINEHIP_FINE_TAIL      nonces at the end of each full-L bucket planned at L - 1 (default
 //                          2^28; 0: none)
 //   MINEHIP_QUEUE          1: fast launches as work queues (workgroups claim chunks, so faster
@@ -313,7 +306,7 @@ mh::PlanOpts plan_opts() {
     }
     if (const char* e = getenv("MINEHIP_STREAMS")) {
         const int v = atoi(e);
-        if (v >= 1 && v <= 3) o.streams = v;
+        if (v == 1 || v == 2) o.streams = v;
     }
     if (const char* e = getenv("MINEHIP_FINE_TAIL")) o.fine_tail = strtoull(e, nullptr, 10);
     if (const char* e = getenv("MINEHIP_QUEUE")) {
@@ -354,14 +347,12 @@ int search_impl(int dev, const mh::Prefix& pre, uint64_t lower, uint64_t upper, 
     // plan is streamed, never stored (a range can hold ~2^30 pieces); this first pass stops as
     // soon as it has seen both kinds.
     bool any_coarse = false, any_fine = false;
-    if (opt.streams >= 2)
+    if (opt.streams == 2)
         mh::plan_search(pre, lower, upper, opt, [&](const mh::Piece& p) {
             (coarse_piece(p, opt) ? any_coarse : any_fine) = true;
             return !(any_coarse && any_fine);
         });
-    const bool split = opt.streams >= 2 && any_coarse && any_fine;
-    c->nps = opt.streams == 3 ? 3 : 2;
-    c->coarse_k = 0;
+    const bool split = opt.streams == 2 && any_coarse && any_fine;
     if (split) {  // the piece streams start after the reset (and after the previous search)
         rc = piece_streams_wait_main(c);
         if (rc) return rc;

@@ -80,7 +80,7 @@ struct PlanOpts {
     // Round 3 (profiles/r03d_*): 2 streams + a 2^28-nonce tail against one stream,
     // wall clock, A/B in one process: configs[1] +1.6%, configs[2] +1.0% / +1.1%, an 8-GPU
     // configs[3] shard +0.2%, and the predicted 8-GPU per-GPU efficiency 0.982 -> 1.00.
-    int streams = 2;  // 3: experiment, consecutive coarse pieces on two high-priority streams
+    int streams = 2;
     uint64_t fine_tail = 1ull << 28;
     // Work queue (execution): a fast launch's workgroups claim 256-run chunks from a counter
     // instead of one chunk each, so the 8 XCDs, whose clocks differ by a few percent, finish
