@@ -131,10 +131,10 @@ __device__ __forceinline__ void sha256_block_kw_last(const uint32_t st[8], const
 }
 }  // namespace dev
 
-// spread(x, k) = x with a zero decimal digit inserted at digit index k (k >= 20: x itself), by
-// divisions by the constant 10 (no general 64-bit division); on the rare new-best branch of the
-// Early modes only
-__device__ __forceinline__ uint64_t spread(uint64_t x, uint32_t k) {
+// spread(x, k, w) = x with w zero decimal digits inserted at digit index k (k >= 20: x itself),
+// by divisions by the constant 10 (no general 64-bit division); on the rare new-best branch of
+// the Early modes only
+__device__ __forceinline__ uint64_t spread(uint64_t x, uint32_t k, uint32_t w) {
     if (k >= 20u) return x;
     uint64_t lo = 0, p = 1;
     for (uint32_t j = 0; j < k; ++j) {
@@ -143,24 +143,25 @@ __device__ __forceinline__ uint64_t spread(uint64_t x, uint32_t k) {
         p *= 10u;
         x = q;
     }
-    return x * p * 10u + lo;
+    for (uint32_t j = 0; j < w; ++j) p *= 10u;
+    return x * p + lo;
 }
 
 // One workgroup-sized chunk: the 256 runs u_start + 256 * blk + threadIdx.x, their minimum
 // written to partials[blk].
 // MODE % 3 is the tail layout (One, Pre, Two); MODE >= 3 (Early): the per-nonce digit ends word
-// J and the group digits lie in words J and J + 1, so word J + 1 is the group-level word and
-// rounds 0..J-1 are all run-level; otherwise the per-nonce digit is the last one (word J) and
-// the group digits lie in words J - 1 and J.
+// J and the group digits sit right before it in word J, so no word but J changes inside a run:
+// rounds 0..J-1 and every schedule word that does not depend on W[J] are run-level; otherwise
+// the per-nonce digit is the last one (word J) and the group digits lie in words J - 1 and J.
 template <int J, int MODE>
 __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restrict__ partials, const uint32_t blk) {
     using namespace dev;
     constexpr uint32_t K[64] = MH_K256;
     constexpr int BM = MODE % 3;                          // tail layout
     constexpr bool EARLY = MODE >= 3;
-    constexpr int JG = EARLY ? J + 1 : J - 1;             // the other word of the group digits
+    constexpr int JG = EARLY ? J : J - 1;                 // the other word of the group digits
     constexpr uint64_t NM = Dep::from(J);                 // nonce-level words
-    constexpr uint64_t GM = Dep::from(JG) & ~NM;          // group-level words
+    constexpr uint64_t GM = Dep::from(JG) & ~NM;          // group-level words (Early: none)
     constexpr int BASE = (BM == kModePre) ? 16 : 0;       // per-nonce block inside the tail
 #define MH_N(t) ((NM >> (t)) & 1ull)
 #define MH_G(t) ((GM >> (t)) & 1ull)
@@ -170,8 +171,8 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
 
     // ---- per run --------------------------------------------------------
     // Tail words: host template + the d-L digits of U, right-aligned so U's
-    // last digit sits at tail byte hi_end-1 (Early: skipping the innermost
-    // digit's byte).  Only words up to the last lower digit's can receive them
+    // last digit sits at tail byte hi_end-1 (Early: skipping the L enumerated
+    // digits' bytes).  Only words up to the last digit's can receive them
     // (words <= BASE + J, Early BASE + J + 1).
     constexpr int JM = EARLY ? J + 1 : J;                 // the last per-lane word
     constexpr int NW = BASE + JM + 1;
@@ -187,7 +188,7 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
                 const uint32_t dg = (uint32_t)(u - q * 10u);
                 u = q;
                 uint32_t pos = a.hi_end - 1u - (uint32_t)k;
-                if constexpr (EARLY) pos -= ((uint32_t)k >= a.hole) ? 1u : 0u;
+                if constexpr (EARLY) pos -= ((uint32_t)k >= a.hole) ? a.hole_w : 0u;
                 add_word(w, pos >> 2, dg << (24u - 8u * (pos & 3u)));
             }
         }
@@ -254,8 +255,8 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
 
     for (uint32_t g = 0; g < a.n_groups; ++g) {
         // ---- per group of 10 nonces --------------------------------------
-        // the L-1 digits of g: wave-uniform, so this is SALU work.  Into word J (cj) or the
-        // other group word JG (cjm)
+        // the L-1 digits of g: wave-uniform, so this is SALU work.  Into word J (cj) or word
+        // J - 1 (cjm; the Early layouts put every group digit in word J)
         uint32_t cj = 0u, cjm = 0u, gq = g;
         if constexpr (!EARLY) {
             // digits 0..L-2 of q = 10*g + i, at bytes lo_pos .. lo_pos+L-2
@@ -288,7 +289,7 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
         const uint32_t wJ = W[J] + cj;  // word J with this group's digits, the per-nonce digit '0'
         const uint32_t s0wJ = ssig0(wJ), s1wJ = ssig1(wJ);
         uint32_t wg[64], pg[64];
-        if constexpr (JG >= 0) wg[JG] = W[JG] + cjm;
+        if constexpr (!EARLY && J > 0) wg[J - 1] = W[J - 1] + cjm;
 #pragma unroll
         for (int t = 16; t < 64; ++t) {
             if (MH_R(t)) continue;
@@ -375,7 +376,8 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
                     if constexpr (!EARLY)
                         cn = (wave_u0 + l) * a.pow10L + q;
                     else
-                        cn = spread(wave_u0 + l, a.hole) * a.u_mul + spread(g, a.g_hole) + i * a.i_mul;
+                        cn = spread(wave_u0 + l, a.hole, a.hole_w) * a.u_mul + spread(g, a.g_hole, 1u) * a.g_mul +
+                             i * a.i_mul;
                     if (c0 < wbh0 || (c0 == wbh0 && (c1 < wbh1 || (c1 == wbh1 && cn < wbn)))) {
                         wbh0 = c0;
                         wbh1 = c1;

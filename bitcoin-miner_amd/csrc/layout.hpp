@@ -30,11 +30,12 @@ enum FastMode : uint32_t {
     kModeTwo = 2,   // two tail blocks; the lower digits sit in block 0 -> both blocks per nonce
     // The same three tail layouts with an earlier innermost digit (mode - 3 is the tail layout):
     // the digit enumerated per nonce is not the last one but the digit ending word J, the word
-    // before the last digit's, and the other lower digits (a group, per 10 nonces) sit in words
-    // J and J + 1.  A nonce then costs nonce_cost(J) instead of nonce_cost(J + 1), which is less
-    // for J + 1 = 1 (W[1] reaches W[16] through sigma0), J + 1 = 9 (W[9] is W[16]'s t-7 term)
-    // and J + 1 = 14.  With the innermost digit at decimal position p >= L a
-    // lane's nonces are not contiguous: its U digits skip position p.
+    // before the last digit's, at decimal position p = 1..4, and the other enumerated digits (a
+    // group, per 10 nonces) are the L - 1 right before it in word J.  A nonce then costs
+    // nonce_cost(J) instead of nonce_cost(J + 1), which is less for J + 1 = 1 (W[1] reaches W[16]
+    // through sigma0), J + 1 = 9 (W[9] is W[16]'s t-7 term) and J + 1 = 14, and
+    // only word J changes inside a lane.  A lane's nonces are not contiguous: its U digits are the
+    // p below and the ones above the L enumerated positions p .. p+L-1.
     kModeOneEarly = 3,
     kModePreEarly = 4,
     kModeTwoEarly = 5,
@@ -57,15 +58,19 @@ struct FastArgs {
     uint32_t mode;        // FastMode
     uint32_t n_chunks;    // workgroup-sized chunks (256 runs each) in this launch
     // Early modes only (the per-run digit formatting and the nonce of a candidate):
-    //   U's digit k sits at tail byte hi_end - 1 - k - (k >= hole), the group's digit j at
-    //   per-nonce-block byte g_last - j - (j >= g_hole), the innermost digit at byte `inner`;
-    //   nonce(U, g, i) = spread(U, hole) * u_mul + spread(g, g_hole) + i * i_mul, where
-    //   spread(x, k) inserts a zero decimal digit at digit index k (k >= 20: x itself).
+    //   U's digit k sits at tail byte hi_end - 1 - k - (k >= hole ? hole_w : 0), the group's
+    //   digit j at per-nonce-block byte g_last - j - (j >= g_hole), the innermost digit at byte
+    //   `inner`; nonce(U, g, i) = spread(U, hole, hole_w) * u_mul + spread(g, g_hole, 1) * g_mul
+    //   + i * i_mul, where spread(x, k, w) inserts w zero decimal digits at digit index k
+    //   (k >= 20: x itself).
     uint32_t inner;
     uint32_t hole;
     uint32_t g_last;
     uint32_t g_hole;
+    uint32_t hole_w;
+    uint32_t pad_;
     uint64_t u_mul;
+    uint64_t g_mul;
     uint64_t i_mul;
     uint32_t kw1[64];     // kModeTwo: K[i] + W[i] of tail block 1 (padding + length only)
     // Work queue: non-null -> the launch's workgroups claim chunks from this zeroed device

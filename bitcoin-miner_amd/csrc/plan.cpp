@@ -196,7 +196,8 @@ bool make_fast_args(const Prefix& pre, int d, int L, bool early, int* J_out, int
     } else if (pl >= 64u) {
         mode = kModePre;
         base = 64;
-        if (pl - (uint32_t)L + 1u < 64u) return false;  // every lower digit must sit in block 1
+        // every enumerated digit must sit in block 1 (the Early layouts check theirs below)
+        if (!early && pl - (uint32_t)L + 1u < 64u) return false;
     } else {
         mode = kModeTwo;
         base = 0;
@@ -212,11 +213,10 @@ bool make_fast_args(const Prefix& pre, int d, int L, bool early, int* J_out, int
         if (ib < t || ib < base) return false;  // no digit there, or not in the per-nonce block
         p = pl - ib;
         if (p < 1u || p >= (uint32_t)d) return false;
-        // the group digits (the L-1 lowest positions other than p) in words J-1 and J
-        for (uint32_t j = 0; j + 1u < (uint32_t)L; ++j) {
-            const uint32_t pos = j + ((p < (uint32_t)L && j >= p) ? 1u : 0u);
-            if (pl - pos < base || (int)((pl - pos - base) >> 2) < J - 1) return false;
-        }
+        // the group digits right before the innermost one, in its word (positions p+1 .. p+L-1):
+        // the group then changes word J-1 only and no schedule word is group-level
+        if (L > 4 || p + (uint32_t)L > (uint32_t)d || ib - (uint32_t)(L - 1) < t || ib - (uint32_t)(L - 1) < base)
+            return false;
         J -= 1;
         mode += 3;
     }
@@ -240,21 +240,22 @@ bool make_fast_args(const Prefix& pre, int d, int L, bool early, int* J_out, int
     fa->mode = (uint32_t)mode;
     fa->hole = kNoHole;
     fa->g_hole = kNoHole;
+    fa->hole_w = 1;
+    fa->g_mul = 1;
     uint64_t block = kPow10[L];
     if (early) {
-        // positions 0..L-2 other than p: the group; the rest, p excluded: U, from the lowest
         fa->inner = ib - base;
-        fa->g_last = pl - base;
         fa->i_mul = kPow10[p];
-        if (p < (uint32_t)L) {  // contiguous lanes: U at positions L.., the group around p
-            fa->g_hole = p;
-            fa->u_mul = kPow10[L];
-        } else {                // U at positions L-1.. skipping p: lanes of one block interleave
-            fa->hi_end = total - (uint32_t)L + 1u;
-            fa->hole = p - (uint32_t)(L - 1);
-            fa->u_mul = kPow10[L - 1];
-            block = kPow10[p + 1u];
-        }
+        // positions p..p+L-1 enumerated (p: per nonce, p+1..: the group), U around them: its low
+        // p digits, then its high digits from position p+L; a block of 10^(p+L) nonces is 10^p
+        // interleaved lanes
+        fa->g_last = ib - 1u - base;
+        fa->hi_end = total;
+        fa->hole = p;
+        fa->hole_w = (uint32_t)L;
+        fa->u_mul = 1;
+        fa->g_mul = kPow10[p + 1u];
+        block = kPow10[p + (uint32_t)L];
     }
     *block_out = block;
     if (mode % 3 == kModeTwo) {
@@ -451,6 +452,53 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         }
     };
 
+    // blocks [ua, ub) of Bx nonces of bucket d, each 10^Lx-nonce lanes [ua * lpb, ub * lpb)
+    auto emit_runs = [&](int d, unsigned __int128 ua, unsigned __int128 ub, uint64_t Bx, int Lx, int Jx, int modex,
+                         int nbx, const FastArgs& fax) -> bool {
+        const unsigned __int128 Rx = kPow10[Lx];
+        const uint64_t lpb = Bx / (uint64_t)Rx;  // lanes per block
+        uint64_t max_runs = std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx);
+        max_runs = std::max<uint64_t>(lpb, max_runs / lpb * lpb);  // whole blocks per launch
+        ua *= lpb;
+        ub *= lpb;
+        for (unsigned __int128 u = ua; u < ub;) {
+            const unsigned __int128 left = ub - u;
+            const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
+            Piece p;
+            memset(&p, 0, sizeof p);
+            p.first = (uint64_t)(u * Rx);
+            p.count = (uint64_t)((unsigned __int128)runs * Rx);
+            p.kind = 0;
+            p.digits = d;
+            p.L = Lx;
+            p.J = Jx;
+            p.mode = modex;
+            p.blocks = nbx;
+            p.fa = fax;
+            { const NonceCost nc = nonce_cost(Jx, modex); p.ops = nc.ops; p.slots = nc.slots; }
+            p.fa.u_start = (uint64_t)u;
+            p.fa.n_runs = (uint32_t)runs;
+            p.ga = gbase;
+            if (!flush_generic() || !cb(p)) return false;
+            u += runs;
+        }
+        return true;
+    };
+    // [a, b] (a <= b) of bucket d outside the whole blocks of an Early layout: the runs of 10^L
+    // nonces of the last-digit layout, the ragged rest on the generic kernel
+    auto emit_edge = [&](int d, uint64_t a, uint64_t b, int L) -> bool {
+        FastArgs fs;
+        int Js = 0, ms = 0, nbs = 1;
+        uint64_t bs = 1;
+        if (!make_fast_args(pre, d, L, false, &Js, &ms, &nbs, &bs, &fs)) return emit_generic(a, b, d);
+        const unsigned __int128 R = bs;
+        const unsigned __int128 u0 = ((unsigned __int128)a + R - 1u) / R, u1 = ((unsigned __int128)b + 1u) / R;
+        if (u0 >= u1) return emit_generic(a, b, d);
+        if (a < (uint64_t)(u0 * R) && !emit_generic(a, (uint64_t)(u0 * R) - 1u, d)) return false;
+        if (!emit_runs(d, u0, u1, bs, L, Js, ms, nbs, fs)) return false;
+        return u1 * R > (unsigned __int128)b || emit_generic((uint64_t)(u1 * R), b, d);
+    };
+
     for (int d = d_lo; d <= d_hi; ++d) {
         const uint64_t A = std::max(lower, bucket_lo(d)), B = std::min(upper, bucket_hi(d));
         FastArgs fa;
@@ -460,19 +508,21 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
             if (!emit_generic(A, B, d)) return;
             continue;
         }
-        // whole blocks of lanes: a block is one run of 10^L nonces, or (an Early layout with the
-        // innermost digit at position p >= L) the 10^(p+1) nonces its 10^(p+1-L) lanes interleave
+        // whole blocks of lanes: a block is one run of 10^L nonces, or (an Early layout) the
+        // 10^(p+L) nonces its 10^p lanes interleave; an Early layout's ragged ends go to the
+        // last-digit layout's runs first (emit_edge)
+        const bool early = mode >= 3;
         const unsigned __int128 R = blk;
         const unsigned __int128 U0 = ((unsigned __int128)A + R - 1u) / R;
         const unsigned __int128 U1p = ((unsigned __int128)B + 1u) / R;  // one past the last full block
         if (U0 >= U1p) {
-            if (!emit_generic(A, B, d)) return;
+            if (!(early ? emit_edge(d, A, B, L) : emit_generic(A, B, d))) return;
             continue;
         }
         const uint64_t fast_first = (uint64_t)(U0 * R);
         const unsigned __int128 fast_end = U1p * R;  // exclusive, may be 2^64
-        if (A < fast_first && !emit_generic(A, fast_first - 1u, d)) return;
-        if (!flush_generic()) return;
+        if (A < fast_first && !(early ? emit_edge(d, A, fast_first - 1u, L) : emit_generic(A, fast_first - 1u, d)))
+            return;
         // Tail split (opt.fine_tail): the last runs of a full-L bucket at L - 1, so that their
         // short workgroups can back-fill the drain of the coarse launches (streams = 2).
         unsigned __int128 U_split = U1p;  // coarse blocks [U0, U_split), then the tail at L - 1
@@ -487,42 +537,12 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
                 Lf = L - 1;
             }
         }
-        // blocks [ua, ub) of Bx nonces, each 10^Lx-nonce lanes [ua * lpb, ub * lpb)
-        auto emit_runs = [&](unsigned __int128 ua, unsigned __int128 ub, uint64_t Bx, int Lx, int Jx, int modex,
-                             int nbx, const FastArgs& fax) -> bool {
-            const unsigned __int128 Rx = kPow10[Lx];
-            const uint64_t lpb = Bx / (uint64_t)Rx;  // lanes per block
-            uint64_t max_runs = std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx);
-            max_runs = std::max<uint64_t>(lpb, max_runs / lpb * lpb);  // whole blocks per launch
-            ua *= lpb;
-            ub *= lpb;
-            for (unsigned __int128 u = ua; u < ub;) {
-                const unsigned __int128 left = ub - u;
-                const uint64_t runs = (left > max_runs) ? max_runs : (uint64_t)left;
-                Piece p;
-                memset(&p, 0, sizeof p);
-                p.first = (uint64_t)(u * Rx);
-                p.count = (uint64_t)((unsigned __int128)runs * Rx);
-                p.kind = 0;
-                p.digits = d;
-                p.L = Lx;
-                p.J = Jx;
-                p.mode = modex;
-                p.blocks = nbx;
-                p.fa = fax;
-                { const NonceCost nc = nonce_cost(Jx, modex); p.ops = nc.ops; p.slots = nc.slots; }
-                p.fa.u_start = (uint64_t)u;
-                p.fa.n_runs = (uint32_t)runs;
-                p.ga = gbase;
-                if (!cb(p)) return false;
-                u += runs;
-            }
-            return true;
-        };
-        if (!emit_runs(U0, U_split, blk, L, J, mode, nb, fa)) return;
-        if (U_split < U1p && !emit_runs(U_split * (R / blkf), U1p * (R / blkf), blkf, Lf, Jf, modef, nbf, faf))
+        if (!emit_runs(d, U0, U_split, blk, L, J, mode, nb, fa)) return;
+        if (U_split < U1p && !emit_runs(d, U_split * (R / blkf), U1p * (R / blkf), blkf, Lf, Jf, modef, nbf, faf))
             return;
-        if (fast_end <= (unsigned __int128)B && !emit_generic((uint64_t)fast_end, B, d)) return;
+        if (fast_end <= (unsigned __int128)B &&
+            !(early ? emit_edge(d, (uint64_t)fast_end, B, L) : emit_generic((uint64_t)fast_end, B, d)))
+            return;
     }
     flush_generic();
 }

@@ -69,7 +69,7 @@ static uint64_t interesting_u64() {
 // per-run formatting of U, the group digits and the per-nonce digit, restated from fast_search.hip
 // on the host), read back as a decimal number, must be the nonce its candidate formula reports,
 // inside the piece -- for the last-digit layouts and the Early ones (interleaved lanes included).
-static uint64_t spread(uint64_t x, uint32_t k) {  // fast_search.hip spread()
+static uint64_t spread(uint64_t x, uint32_t k, uint32_t w) {  // fast_search.hip spread()
     if (k >= 20u) return x;
     uint64_t lo = 0, q = 1;
     for (uint32_t j = 0; j < k; ++j) {
@@ -77,7 +77,8 @@ static uint64_t spread(uint64_t x, uint32_t k) {  // fast_search.hip spread()
         q *= 10u;
         x /= 10u;
     }
-    return x * q * 10u + lo;
+    for (uint32_t j = 0; j < w; ++j) q *= 10u;
+    return x * q + lo;
 }
 static uint64_t g_fast_checked = 0, g_early_checked = 0;
 static bool lanes_format_their_nonces(const mh::Prefix& pre, const mh::Piece& p) {
@@ -95,7 +96,7 @@ static bool lanes_format_their_nonces(const mh::Prefix& pre, const mh::Piece& p)
         for (uint32_t x = 0; x < 128; ++x) b[x] = (uint8_t)(a.blk[x >> 2] >> (24u - 8u * (x & 3u)));
         uint64_t u = U;
         for (uint32_t k = 0; k < a.n_hi; ++k, u /= 10u)
-            b[a.hi_end - 1u - k - ((early && k >= a.hole) ? 1u : 0u)] += (uint8_t)(u % 10u);
+            b[a.hi_end - 1u - k - ((early && k >= a.hole) ? a.hole_w : 0u)] += (uint8_t)(u % 10u);
         uint32_t gq = g;
         for (uint32_t j = 0; j + 1u < a.L; ++j, gq /= 10u) {
             const uint32_t pos = early ? a.g_last - j - (j >= a.g_hole ? 1u : 0u) : a.lo_pos + (a.L - 2u - j);
@@ -108,7 +109,7 @@ static bool lanes_format_their_nonces(const mh::Prefix& pre, const mh::Piece& p)
             if (c < '0' || c > '9' || (x == 0 && c == '0' && d > 1)) return false;
             n = n * 10u + (uint64_t)(c - '0');
         }
-        const uint64_t want = early ? spread(U, a.hole) * a.u_mul + spread(g, a.g_hole) + i * a.i_mul
+        const uint64_t want = early ? spread(U, a.hole, a.hole_w) * a.u_mul + spread(g, a.g_hole, 1) * a.g_mul + i * a.i_mul
                                     : U * a.pow10L + (uint64_t)g * 10u + i;
         if (n != want || n < p.first || n - p.first >= p.count) return false;
     }

@@ -130,9 +130,9 @@ def check_plan(msg, lo, hi):
                 assert ((pl - base - L + 1) >> 2) >= p["word"] - 1
             else:  # Early: the innermost digit ends word J, the word before the last digit's
                 assert p["word"] == ((pl - base) >> 2) - 1
-                pos = pl - (base + 4 * p["word"] + 3)  # its decimal position
-                assert 1 <= pos < d
-                block = 10 ** max(L, pos + 1)
+                pos = pl - (base + 4 * p["word"] + 3)  # its decimal position; the group's: pos+1..
+                assert 1 <= pos and pos + L <= d and pl - pos - (L - 1) >= max(t, base)
+                block = 10 ** (pos + L)
                 assert p["first"] % block == 0 and p["count"] % block == 0  # whole blocks of lanes
             if mode == 1:
                 assert pl - L + 1 >= 64
@@ -359,7 +359,7 @@ def test_embedded_code_object_carries_queue_marker():
     md = codeobj.metadata(co)
     fast = [k for k in md["amdhsa.kernels"] if "fast_search" in k[".name"]]
     assert len(fast) == len(KERNELS)
-    assert {k[".args"][0][".size"] for k in fast} == {504}      # FastArgs, by value
+    assert {k[".args"][0][".size"] for k in fast} == {520}      # FastArgs, by value
     nomarker = os.path.join(ROOT, "build", "fast_search_nomarker.hsaco")
     if os.path.exists(nomarker):
         assert b"mh_fast_queue_args" not in open(nomarker, "rb").read()

@@ -98,7 +98,7 @@ def test_config3_fixture():
 
 
 # the last-digit layouts an Early layout replaces in the default plan of every bucket holding two
-# blocks of its lanes (<= 2 x 10^5 nonces); MINEHIP_EARLY=0 plans them instead
+# blocks of its lanes (10^(p+L) nonces each, up to 10^7); MINEHIP_EARLY=0 plans them instead
 REPLACED_BY_EARLY = {(1, 0), (1, 1), (9, 0), (14, 2)}
 EARLY_FIXTURES = ("cfg3b", "two14", "two15", "pre2", "one1", "one10")
 
@@ -132,7 +132,8 @@ def test_fixtures_cover_every_fast_layout():
     the same fixtures plan with MINEHIP_EARLY=0 (tests/test_gpu_fullsize.py runs both)."""
     from test_abi import KERNELS
     used = _used(CFGS, 1)
-    assert used == KERNELS - {(0, 0)} - REPLACED_BY_EARLY, sorted(KERNELS - used)
+    # (the replaced kernels may still run an Early bucket's ragged ends, in runs of 10^L)
+    assert KERNELS - {(0, 0)} - REPLACED_BY_EARLY <= used <= KERNELS - {(0, 0)}, sorted(KERNELS - used)
     assert _used(EARLY_FIXTURES, 0) >= REPLACED_BY_EARLY
     for name in EARLY_FIXTURES:  # exactly these fixtures change kernels with the knob
         assert _used((name,), 1) != _used((name,), 0), name

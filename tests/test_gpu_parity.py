@@ -127,7 +127,8 @@ def test_every_kernel_instantiation(gpu):
 def early_position_cases(Ls=(1, 2, 3)):
     """(msg, lo, hi, L, J, mode, p) for every (Early kernel, innermost position p, L) the planner
     can produce: messages of every tail offset, each bucket d = 2..20 from its first nonce (and
-    the top of the u64 range for d = 20), two blocks of lanes plus a ragged edge.  Host only."""
+    the top of the u64 range for d = 20), two blocks of lanes (10^(p+L) nonces each) plus a
+    ragged edge.  Host only."""
     import minehip
     cases = {}
     for n in range(0, 128):
@@ -136,16 +137,17 @@ def early_position_cases(Ls=(1, 2, 3)):
         for d in range(2, 21):
             for Ld in Ls:
                 with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
-                    los = [10 ** (d - 1)] + ([U64 - 250_000] if d == 20 else [])
+                    size = 2 * 10 ** (4 + Ld) + 3_456  # two blocks at p = 4
+                    los = [10 ** (d - 1)] + ([U64 - size] if d == 20 else [])
                     for lo in los:
-                        hi = min(U64, lo + 2 * 10 ** 5 + 3_456)
+                        hi = min(U64, lo + size)
                         for pc in minehip.plan(m, lo, hi):
                             if pc["kind"] != 0 or pc["mode"] < 3:
                                 continue
                             pl = t + pc["digits"] - 1
                             base = 64 if (pc["blocks"] == 2 and pl >= 64) else 0
                             pos = pl - (base + 4 * pc["word"] + 3)
-                            assert 1 <= pos <= 4, (n, lo, pc)
+                            assert 1 <= pos <= 4 and pc["first"] % 10 ** (pos + pc["lo_digits"]) == 0, (n, lo, pc)
                             key = (pc["word"], pc["mode"], pos, pc["lo_digits"], lo == los[-1] and d == 20)
                             cases.setdefault(key, (m, lo, hi, Ld))
     return cases
