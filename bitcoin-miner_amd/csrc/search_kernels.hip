@@ -250,11 +250,10 @@ hipError_t launch_fast(int dev, int J, int mode, const FastArgs& a, Partial* par
     if (!fast_variant_exists(J, mode)) return hipErrorInvalidValue;
 #ifdef MH_DEV_HOOKS
     // MINEHIP_DEV_LDS (dev build only): reserve dynamic LDS per workgroup to
-    // cap occupancy, e.g. 54000 -> 3 workgroups (waves/SIMD) per CU.
-    static const unsigned lds = [] {
-        const char* e = getenv("MINEHIP_DEV_LDS");
-        return e ? (unsigned)atoi(e) : 0u;
-    }();
+    // cap occupancy, e.g. 54000 -> 3 workgroups (waves/SIMD) per CU.  Read at every launch, so
+    // that one A/B process can interleave settings.
+    const char* lds_env = getenv("MINEHIP_DEV_LDS");
+    const unsigned lds = lds_env ? (unsigned)atoi(lds_env) : 0u;
 #else
     constexpr unsigned lds = 0;
 #endif
