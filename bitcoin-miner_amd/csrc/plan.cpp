@@ -484,12 +484,15 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         }
         return true;
     };
-    // [a, b] (a <= b) of bucket d outside the whole blocks of an Early layout: the runs of 10^L
-    // nonces of the last-digit layout, the ragged rest on the generic kernel
-    auto emit_edge = [&](int d, uint64_t a, uint64_t b, int L) -> bool {
+    // [a, b] (a <= b) of bucket d outside the whole blocks of an Early layout (< 10^(p+L) nonces
+    // at each end): 10-nonce runs of the last-digit layout -- short workgroups, on the low-
+    // priority stream, so that an edge never ends a search with a few 1,000-nonce lanes -- and
+    // the ragged rest on the generic kernel
+    auto emit_edge = [&](int d, uint64_t a, uint64_t b) -> bool {
         FastArgs fs;
         int Js = 0, ms = 0, nbs = 1;
         uint64_t bs = 1;
+        const int L = 1;
         if (!make_fast_args(pre, d, L, false, &Js, &ms, &nbs, &bs, &fs)) return emit_generic(a, b, d);
         const unsigned __int128 R = bs;
         const unsigned __int128 u0 = ((unsigned __int128)a + R - 1u) / R, u1 = ((unsigned __int128)b + 1u) / R;
@@ -516,12 +519,12 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const unsigned __int128 U0 = ((unsigned __int128)A + R - 1u) / R;
         const unsigned __int128 U1p = ((unsigned __int128)B + 1u) / R;  // one past the last full block
         if (U0 >= U1p) {
-            if (!(early ? emit_edge(d, A, B, L) : emit_generic(A, B, d))) return;
+            if (!(early ? emit_edge(d, A, B) : emit_generic(A, B, d))) return;
             continue;
         }
         const uint64_t fast_first = (uint64_t)(U0 * R);
         const unsigned __int128 fast_end = U1p * R;  // exclusive, may be 2^64
-        if (A < fast_first && !(early ? emit_edge(d, A, fast_first - 1u, L) : emit_generic(A, fast_first - 1u, d)))
+        if (A < fast_first && !(early ? emit_edge(d, A, fast_first - 1u) : emit_generic(A, fast_first - 1u, d)))
             return;
         // Tail split (opt.fine_tail): the last runs of a full-L bucket at L - 1, so that their
         // short workgroups can back-fill the drain of the coarse launches (streams = 2).
@@ -541,7 +544,7 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         if (U_split < U1p && !emit_runs(d, U_split * (R / blkf), U1p * (R / blkf), blkf, Lf, Jf, modef, nbf, faf))
             return;
         if (fast_end <= (unsigned __int128)B &&
-            !(early ? emit_edge(d, (uint64_t)fast_end, B, L) : emit_generic((uint64_t)fast_end, B, d)))
+            !(early ? emit_edge(d, (uint64_t)fast_end, B) : emit_generic((uint64_t)fast_end, B, d)))
             return;
     }
     flush_generic();
