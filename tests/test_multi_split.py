@@ -95,7 +95,14 @@ def test_split_argument_errors():
         minehip.multi_plan(b"x", 0, 4, minehip._lib.MH_MAX_WORKERS + 1)
     assert e.value.code == minehip.MH_EINVAL
     assert len(minehip.multi_plan(b"x", 0, 10 ** 6, minehip._lib.MH_MAX_WORKERS)) == minehip._lib.MH_MAX_WORKERS
+    # a weight per worker, no more and no fewer (a short list was zero-padded by ctypes)
+    for w in ([1.0], [1.0, 1.0, 1.0]):
+        with pytest.raises(ValueError):
+            minehip.multi_plan(b"x", 0, 4, 2, w)
 
 
 def test_rate_table_starts_empty():
     assert minehip.multi_rates([0, 1, 7]) == [0.0, 0.0, 0.0]
+    # an empty device list is no error, whatever the pointers
+    assert minehip.lib.mh_multi_rates(None, 0, None) == 0
+    assert minehip.multi_rates([]) == []
