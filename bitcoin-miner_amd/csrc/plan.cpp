@@ -180,8 +180,8 @@ bool kernel_exists(int J, int mode) {
 
 // Fast-kernel launch template for bucket d with L lower digits.  early: the digit ending the word
 // before the last digit's is enumerated innermost (layout.hpp kMode*Early) -- false when the
-// layout does not allow it.  *block_out: the nonces of one block of lanes (10^L, or 10^(p+1)
-// when the innermost digit sits at decimal position p >= L), the unit a piece is cut in.
+// layout does not allow it.  *block_out: the nonces of one block of lanes, the unit a piece is cut
+// in: 10^L, or for an Early layout 10^(p+L) (p: the innermost digit's decimal position).
 bool make_fast_args(const Prefix& pre, int d, int L, bool early, int* J_out, int* mode_out, int* blocks_out,
                     uint64_t* block_out, FastArgs* fa) {
     const uint32_t t = pre.t;
