@@ -886,7 +886,10 @@ def main():
         pipe.nonces = 0
     n1 = None
     if n_gpus > 1 and not args.no_n1:
-        # the same workload on device 0 alone, before the timed region (the other ranks wait)
+        # the same workload on device 0 alone, before the timed region (the other ranks wait); the
+        # first barrier lets every rank's warmup searches end first (on a one-GPU rehearsal they
+        # would otherwise share rank 0's device during its search)
+        barrier()
         if rank == 0:
             n1 = same_workload_n1(lambda m, a, b: minehip.search(m, a, b, devs[0]), steps)
         barrier()
