@@ -90,6 +90,12 @@ for s in $STEPS; do
       timeout -k 10 600 python "$ROOT/tools/inproc_model.py" --out "$OUT/inproc_model.json" > "$OUT/inproc.log" 2>&1
       rc=$?; echo "inproc rc=$rc" | tee -a "$OUT/session.log"; cat "$OUT/inproc.log"; fatal $rc
       ;;
+    strong)
+      # the launched N-GPU strong line (configs[3]) predicted on this GPU: every (step, rank) shard
+      # timed alone, step time = the slowest rank's (tools/strong_shards.py)
+      timeout -k 10 900 python "$ROOT/tools/strong_shards.py" --out "$OUT/strong_shards.json" > "$OUT/strong.log" 2>&1
+      rc=$?; echo "strong rc=$rc" | tee -a "$OUT/session.log"; tail -5 "$OUT/strong.log"; fatal $rc
+      ;;
     pmc)
       (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
           -d "$OUT/pmc1" -o run --output-format csv \
