@@ -30,7 +30,7 @@ RPATH   := -Wl,-rpath,'$$ORIGIN/../minehip'
 
 DEVLIB  := $(BUILD)/dev/libminehip.so
 
-all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so $(FAST_MIX) $(BUILD)/fast_search_nomarker.hsaco
+all: $(LIB) $(LSPLIB) $(CLIS) oracle dev $(BUILD)/libclockprobe.so $(BUILD)/libvaluenergy.so $(FAST_MIX) $(BUILD)/fast_search_nomarker.hsaco
 
 # LSP endpoint (host only, wire compatible with the reference's Go lsp package)
 $(LSPLIB): $(CSRC)/lsp/lsp.cpp include/lsp440.h
@@ -97,6 +97,11 @@ $(BUILD)/libclockprobe.so: tools/clock_probe.hip
 	mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
+# energy per VALU instruction class at the power limit (measurement only: tools/energy_probe.py)
+$(BUILD)/libvaluenergy.so: tools/valu_energy.hip
+	mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
+
 # disassembly + register report of the kernels (for DESIGN.md / profiling)
 asm: $(FAST_PS)
 	mkdir -p build
@@ -122,7 +127,7 @@ build/valu_%: tools/valu_%.hip
 
 clean:
 	rm -f $(LIB) $(DEVLIB) $(LSPLIB) $(CLIS) $(FAST_S) $(FAST_SP) $(FAST_PS) $(FAST_MIX) $(FAST_CO) $(FAST_O) \
-	      $(BUILD)/fast_search_prio.o $(BUILD)/libclockprobe.so $(BUILD)/add3_split.*.stamp \
+	      $(BUILD)/fast_search_prio.o $(BUILD)/libclockprobe.so $(BUILD)/libvaluenergy.so $(BUILD)/add3_split.*.stamp \
 	      $(BUILD)/fast_search_nomarker.*
 	$(MAKE) -s -C oracle clean
 

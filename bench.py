@@ -492,13 +492,44 @@ def gpu_config1(search_dev):
     return {"config1_ms": round(sorted(ts)[5] * 1e3, 3), "config1_result": list(r)}
 
 
-def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
+def energy_meter(dev):
+    """tools/energy.py's Meter for HIP device `dev` (amdsmi: the socket's energy counter and the
+    firmware's limit accumulators), or None when the library cannot reach the device."""
+    tools = os.path.join(ROOT, "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    try:
+        import energy
+        m = energy.meter_for_device(dev)
+    except Exception as e:  # a missing amdsmi leaves the energy fields empty, not the line
+        return {"error": f"{type(e).__name__}: {e}"}
+    return m if m.ok else {"error": m.error}
+
+
+def energy_fields(res, kc=None):
+    """The line's energy object from a Window result (and the clock probe of the same search)."""
+    if not res or "joules" not in res:
+        return {"error": (res or {}).get("energy_error") or (res or {}).get("error") or "not measured"}
+    snap = res.get("snapshot", {})
+    out = {"j_per_gnonce": res.get("j_per_gnonce"), "mean_w": res.get("mean_w"),
+           "kernel_clock_ghz": (kc or {}).get("ghz"), "joules": res["joules"], "seconds": res["seconds"],
+           "nonces": res.get("nonces"), "limiter": res.get("limiter"),
+           "limit_active_share": res.get("limit_active_share"),
+           "power_limit_w": snap.get("power_limit_w"), "gfx_voltage_mv": snap.get("voltage_gfx"),
+           "socket_power_w": snap.get("current_socket_power"), "gfx_clk_mhz": snap.get("gfx_clk_mhz"),
+           "throttle_status": snap.get("throttle_status"), "hotspot_c": snap.get("temperature_hotspot")}
+    return out
+
+
+def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=None):
     """The engine clock the fast kernel runs at, read inside the GPU during an un-profiled
     search (tools/clock_probe.hip, build/libclockprobe.so): one-wave probe workgroups on their
     own stream sleep through a 2^37-nonce search of the dominant layout (fast_search<4, One> at
     L = 3) and read the shader-clock and 100 MHz counters at both ends of a window inside it.
     Returns the median clock over the probes, the median per XCD and the search's own rate, or
-    None when the probe library is missing or the window did not lie inside the search."""
+    None when the probe library is missing or the window did not lie inside the search.
+    With `meter` (energy_meter), the same search is bracketed by the socket's energy counter and
+    the limit accumulators: the result's "energy" (J per 10^9 nonces, mean W, the active limit)."""
     import ctypes
     path = os.path.join(ROOT, "build", "libclockprobe.so")
     if not os.path.exists(path):
@@ -510,9 +541,17 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
     if lib.cp_start(dev, delay_s, window_s, nwg) != 0:
         return None
     buf = (ctypes.c_uint64 * (4 * nwg))()
+    win = None
+    if meter is not None and not isinstance(meter, dict):
+        import energy
+        win = energy.Window(meter, nonces=n, snap_after_s=delay_s + window_s / 2)
     try:
         t = time.perf_counter()
-        search_dev("cmu440", lo, lo + n - 1)
+        if win is not None:
+            with win:
+                search_dev("cmu440", lo, lo + n - 1)
+        else:
+            search_dev("cmu440", lo, lo + n - 1)
         search_s = time.perf_counter() - t
     finally:
         rc = lib.cp_read(dev, buf, nwg)  # always: waits for the probes and frees their buffer
@@ -522,7 +561,10 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
     ghz = [(x, c / (k / 1e8) / 1e9) for x, c, k, _ in rows if k]
     late = max(w for *_, w in rows) / 1e8  # window start after the workgroup started, s
     if not ghz or search_s < late + window_s + 0.1:
-        return {"ghz": None, "note": f"probe window not inside the search ({search_s:.2f} s)"}
+        out = {"ghz": None, "note": f"probe window not inside the search ({search_s:.2f} s)"}
+        if win is not None:
+            out["energy"] = energy_fields(win.result)
+        return out
 
     def med(v):
         v = sorted(v)
@@ -531,19 +573,25 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64):
     by_xcd = {}
     for x, g in ghz:
         by_xcd.setdefault(int(x), []).append(g)
-    return {"ghz": round(med([g for _, g in ghz]), 4),
-            "ghz_by_xcd": {str(x): round(med(v), 4) for x, v in sorted(by_xcd.items())},
-            "probes": len(ghz), "window_s": window_s, "search_s": round(search_s, 3),
-            "search_ghs": round(n / search_s / 1e9, 3),
-            "note": "s_memtime / s_memrealtime x 100 MHz in one-wave probe workgroups on their own stream, "
-                    f"window {delay_s}..{delay_s + window_s} s into a 2^37-nonce un-profiled search of "
-                    "fast_search<4, One> (tools/clock_probe.hip)"}
+    out = {"ghz": round(med([g for _, g in ghz]), 4),
+           "ghz_by_xcd": {str(x): round(med(v), 4) for x, v in sorted(by_xcd.items())},
+           "probes": len(ghz), "window_s": window_s, "search_s": round(search_s, 3),
+           "search_ghs": round(n / search_s / 1e9, 3),
+           "note": "s_memtime / s_memrealtime x 100 MHz in one-wave probe workgroups on their own stream, "
+                   f"window {delay_s}..{delay_s + window_s} s into a 2^37-nonce un-profiled search of "
+                   "fast_search<4, One> (tools/clock_probe.hip)"}
+    if meter is not None:
+        out["energy"] = (energy_fields(win.result, out) if win is not None else
+                         {"error": meter.get("error", "no meter")})
+    return out
 
 
-def kernel_clocks(search_on, devices, probe=None):
+def kernel_clocks(search_on, devices, probe=None, meters=None):
     """kernel_clock on every device at once, one host thread per device (the in-process N-GPU
     path): each device runs its own 2^37-nonce search with its probe inside,
-    so the clocks are those of N devices under load together, as in the timed region.
+    so the clocks are those of N devices under load together, as in the timed region.  With
+    `meters` ({dev: energy_meter(dev)}) each device's search is also its energy window (VERDICT r05
+    item 2: per-device power and J per 10^9 nonces beside the clock).
     search_on(dev) -> search_dev for that device.  Returns {dev: kernel_clock result or None}."""
     import threading
     probe = probe or kernel_clock
@@ -551,7 +599,8 @@ def kernel_clocks(search_on, devices, probe=None):
 
     def run(d):
         try:
-            out[d] = probe(search_on(d), d)
+            out[d] = (probe(search_on(d), d) if meters is None else
+                      probe(search_on(d), d, meter=meters.get(d)))
         except Exception as e:  # a failed probe leaves that device's clock unknown, not the line
             out[d] = {"ghz": None, "note": f"probe failed: {e}"}
 
@@ -909,16 +958,21 @@ def main():
         p["elapsed"] = elapsed
     if launched and not args.no_clock:
         # every rank's own GPU clock, read inside the GPU during an un-profiled search run by all
-        # ranks at once after the timed region: what sets the per-GPU rates of a multi-GPU line
-        kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
+        # ranks at once after the timed region: what sets the per-GPU rates of a multi-GPU line;
+        # the same search is the rank's energy window (socket power, J per 10^9 nonces, the limit)
+        kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0],
+                          meter=energy_meter(devs[0]))
         for p in per_dev:
             p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
+            p["energy"] = kc.get("energy") if kc else None
     elif multi and not args.no_clock:
-        # the in-process path: every device's clock at once, one host thread per device
-        kcs = kernel_clocks(lambda d: (lambda m, a, b: minehip.search(m, a, b, d)), uniq)
+        # the in-process path: every device's clock and energy at once, one host thread per device
+        kcs = kernel_clocks(lambda d: (lambda m, a, b: minehip.search(m, a, b, d)), uniq,
+                            meters={d: energy_meter(d) for d in uniq})
         for p in per_dev:
             kc = kcs.get(p["dev"])
             p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
+            p["energy"] = kc.get("energy") if kc else None
 
     t_max = elapsed
     if launched:
@@ -1026,8 +1080,12 @@ def main():
         if n_gpus == 1 and not launched and not args.no_clock:
             # the clock read inside the GPU during an un-profiled search of the same kernel, and the
             # fraction of the issue peak at that clock
-            kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0])
+            kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0],
+                              meter=energy_meter(devs[0]))
             if kc:
+                # energy of the same un-profiled search: J per 10^9 nonces of
+                # fast_search<4, One>, the socket's mean power, and which limit held the clock
+                roof["energy"] = kc.pop("energy", None)
                 roof["kernel_clock"] = kc
                 if kc.get("ghz"):
                     at = kc["ghz"] * 1e9
@@ -1039,12 +1097,17 @@ def main():
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
                        if p["kstats"] and p["kstats"][0]["ns"] else None,
-                       "kernel_clock_ghz": p.get("kernel_clock_ghz")}
+                       "kernel_clock_ghz": p.get("kernel_clock_ghz"),
+                       "energy": p.get("energy")}
                       for p in per_dev]
         if multi:  # the rates the library sized the last step's shards by (cost units per ns)
             for pd, rate in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
                 pd["multi_rate"] = round(rate, 1)
         clocks = [p["kernel_clock_ghz"] for p in per_device if p.get("kernel_clock_ghz")]
+        # per-device socket power and J per 10^9 nonces of the same concurrent search (N > 1): a node
+        # power limit pulling the clocks down shows here, not as scheduling in per_gpu_efficiency
+        watts = [p["energy"]["mean_w"] for p in per_device if (p.get("energy") or {}).get("mean_w")]
+        jpg = [p["energy"]["j_per_gnonce"] for p in per_device if (p.get("energy") or {}).get("j_per_gnonce")]
         line = {
             "metric": METRIC,
             "value": round(value, 4),
@@ -1069,6 +1132,8 @@ def main():
             # the timed region -- with per_gpu_efficiency, whether a shortfall is clock spread between
             # power-limited devices or scheduling
             "kernel_clock_ghz_range": [min(clocks), max(clocks)] if n_gpus > 1 and clocks else None,
+            "power_w_range": [min(watts), max(watts)] if n_gpus > 1 and watts else None,
+            "j_per_gnonce_range": [min(jpg), max(jpg)] if n_gpus > 1 and jpg else None,
             "per_gpu_efficiency": (per_gpu_efficiency(value, n_gpus, n1["ghs"])
                                    if n1 and cfg_name == "4" and args.bits is None and args.msg is None else None),
             "n1_config4": n1,

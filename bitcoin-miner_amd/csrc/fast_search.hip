@@ -273,17 +273,14 @@ __device__ __forceinline__ void fast_chunk(const FastArgs& a, Partial* __restric
             }
         } else {
             // g's digit j (least significant first) at byte g_last - j, one more to the left
-            // from j = g_hole on (the innermost digit's decimal place)
+            // from j = g_hole on (the innermost digit's decimal place); every one in word J
+            // (make_fast_args builds only such pieces, enqueue_piece re-checks each one)
             for (uint32_t j = 0; j + 1u < a.L; ++j) {
                 const uint32_t q = gq / 10u;
                 const uint32_t dg = gq - q * 10u;
                 gq = q;
                 const uint32_t p = a.g_last - j - (j >= a.g_hole ? 1u : 0u);
-                const uint32_t v = dg << (24u - 8u * (p & 3u));
-                if ((p >> 2) == (uint32_t)J)
-                    cj += v;
-                else
-                    cjm += v;
+                cj += dg << (24u - 8u * (p & 3u));
             }
         }
         const uint32_t wJ = W[J] + cj;  // word J with this group's digits, the per-nonce digit '0'
@@ -445,12 +442,7 @@ __device__ __attribute__((used)) uint8_t mh_fast_queue_args[sizeof(FastArgs)];
 // costs less with the digit ending word J innermost than with the last digit
 // in word J + 1 (plan.cpp: nonce_cost(J) < nonce_cost(J + 1)).
 #define MH_INST(j, m) template __global__ void fast_search<j, m>(const FastArgs, Partial* __restrict__);
-MH_INST(0, kModeOne) MH_INST(1, kModeOne) MH_INST(2, kModeOne) MH_INST(3, kModeOne) MH_INST(4, kModeOne)
-MH_INST(5, kModeOne) MH_INST(6, kModeOne) MH_INST(7, kModeOne) MH_INST(8, kModeOne) MH_INST(9, kModeOne)
-MH_INST(10, kModeOne) MH_INST(11, kModeOne) MH_INST(12, kModeOne) MH_INST(13, kModeOne)
-MH_INST(0, kModePre) MH_INST(1, kModePre) MH_INST(2, kModePre) MH_INST(3, kModePre) MH_INST(4, kModePre)
-MH_INST(13, kModeTwo) MH_INST(14, kModeTwo) MH_INST(15, kModeTwo)
-MH_INST(0, kModeOneEarly) MH_INST(8, kModeOneEarly) MH_INST(0, kModePreEarly) MH_INST(13, kModeTwoEarly)
+MH_FAST_KERNELS(MH_INST)  // layout.hpp: the one list of instantiated layouts
 #undef MH_INST
 
 }  // namespace mh

@@ -41,6 +41,34 @@ enum FastMode : uint32_t {
     kModeTwoEarly = 5,
 };
 constexpr int kModes = 6;
+
+// The instantiated fast_search<J, MODE> kernels: every layout a bucket with d <= 20 can produce
+// (One J = 0..13, Pre J = 0..4, Two J = 13..15) and the Early layouts the planner takes (One
+// J = 0, 8, Pre J = 0, Two J = 13).  The one list: fast_search.hip instantiates it, the planner
+// (plan.cpp) and the launcher (search_kernels.hip) accept exactly it, csrc/loop_mix.py and the
+// tests read it from here.
+#define MH_FAST_KERNELS(X)                                                                                 \
+    X(0, kModeOne) X(1, kModeOne) X(2, kModeOne) X(3, kModeOne) X(4, kModeOne) X(5, kModeOne)              \
+    X(6, kModeOne) X(7, kModeOne) X(8, kModeOne) X(9, kModeOne) X(10, kModeOne) X(11, kModeOne)            \
+    X(12, kModeOne) X(13, kModeOne)                                                                        \
+    X(0, kModePre) X(1, kModePre) X(2, kModePre) X(3, kModePre) X(4, kModePre)                             \
+    X(13, kModeTwo) X(14, kModeTwo) X(15, kModeTwo)                                                        \
+    X(0, kModeOneEarly) X(8, kModeOneEarly) X(0, kModePreEarly) X(13, kModeTwoEarly)
+
+struct FastKernelId {
+    int J;
+    int mode;
+};
+#define MH_FAST_KERNEL_ID(j, m) FastKernelId{j, m},
+constexpr FastKernelId kFastKernels[] = {MH_FAST_KERNELS(MH_FAST_KERNEL_ID)};
+#undef MH_FAST_KERNEL_ID
+constexpr int kNumFastKernels = (int)(sizeof(kFastKernels) / sizeof(kFastKernels[0]));
+
+constexpr bool fast_kernel_exists(int J, int mode) {
+    for (const FastKernelId& k : kFastKernels)
+        if (k.J == J && k.mode == mode) return true;
+    return false;
+}
 constexpr uint32_t kNoHole = 20;  // a digit index no layout reaches (d <= 20)
 
 // Arguments of the fast (run) kernel.  Passed by value: lands in SGPRs.

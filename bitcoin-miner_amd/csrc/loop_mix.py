@@ -10,10 +10,9 @@ instructions and the half-rate ones of its per-nonce loop, read from the assembl
 assembled into the embedded code object.  tools/isa_report.py prints the same loops.
 """
 import json
+import os
 import re
 import sys
-
-import os
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from valu_rates import valu_rate  # noqa: E402  (the opcode tables of the issue-priority pass)
@@ -75,11 +74,21 @@ def loop_mix(text):
     return out
 
 
+def fast_kernels(layout=os.path.join(os.path.dirname(os.path.abspath(__file__)), "layout.hpp")):
+    """{(J, MODE)} of layout.hpp's MH_FAST_KERNELS list: the instantiated fast_search layouts."""
+    text = open(layout).read()
+    body = text[text.index("#define MH_FAST_KERNELS(X)"):]
+    body = body[:body.index("\n\n")]
+    modes = {m: int(v) for m, v in re.findall(r"(kMode\w+)\s*=\s*(\d+)", text)}
+    return {(int(j), modes[m]) for j, m in re.findall(r"X\((\d+),\s*(kMode\w+)\)", body)}
+
+
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     mix = loop_mix(open(src).read())
-    if len(mix) != 26 or any(v["valu"] == 0 for v in mix.values()):
-        sys.exit(f"loop_mix: expected 26 fast_search loops in {src}, found {len(mix)}")
+    want = {f"{j},{m}" for j, m in fast_kernels()}
+    if set(mix) != want or any(v["valu"] == 0 for v in mix.values()):
+        sys.exit(f"loop_mix: expected the {len(want)} fast_search loops of layout.hpp in {src}, found {len(mix)}")
     with open(dst, "w") as f:
         json.dump(mix, f, indent=0, sort_keys=True)
     print(f"loop_mix: {len(mix)} per-nonce loops -> {dst}")

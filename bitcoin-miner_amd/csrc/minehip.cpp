@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -206,6 +207,21 @@ int flush_partials(DevCtx* c, bool split) {
 // (shorter lanes, generic edges, the tail split) to the low-priority one.
 bool coarse_piece(const mh::Piece& p, const mh::PlanOpts& opt) { return p.kind == 0 && p.L == opt.lower_digits; }
 
+// An Early piece (layout.hpp kMode*Early) enumerates its innermost digit and the L - 1 group digits
+// before it inside word J: the kernel adds every group digit into word J, so a digit elsewhere
+// would be hashed at the wrong place.  make_fast_args only builds such pieces; this re-checks it
+// where a piece reaches the kernel, with the U digits' hole inside the d digits.
+bool early_piece_ok(const mh::Piece& p) {
+    const mh::FastArgs& a = p.fa;
+    const uint32_t J = (uint32_t)p.J;
+    if ((a.inner >> 2) != J || a.hole + a.hole_w > a.n_hi + a.L) return false;
+    for (uint32_t j = 0; j + 1u < a.L; ++j) {
+        const uint32_t pos = a.g_last - j - (j >= a.g_hole ? 1u : 0u);
+        if (pos > a.g_last || (pos >> 2) != J) return false;
+    }
+    return true;
+}
+
 // Enqueue one piece on the context's stream.  Its workgroups write their
 // partials after those of the previous pieces; one merge folds them all (or
 // earlier, when the buffer would overflow), instead of one merge per piece.
@@ -217,6 +233,8 @@ int enqueue_piece(DevCtx* c, const mh::Piece& p, const mh::PlanOpts& opt, bool s
         // partials buffer holds one slot per block
         if (p.fa.n_runs == 0 || p.fa.L < 1 || p.fa.L > 5 || p.fa.n_hi + p.fa.L > 20)
             return fail(MH_EINTERNAL, "internal: bad fast piece");
+        if (p.fa.mode >= mh::kModeOneEarly && !early_piece_ok(p))
+            return fail(MH_EINTERNAL, "internal: bad Early piece (an enumerated digit outside word J)");
         blocks = (p.fa.n_runs + mh::kBlockThreads - 1) / mh::kBlockThreads;
     } else {
         if (p.ga.count == 0 || p.ga.count > (uint64_t)mh::kMaxBlocksPerLaunch * mh::kBlockThreads)
@@ -429,10 +447,23 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
     // MINEHIP_TEST_FAIL_WORKER=i makes worker i's first search fail with
     // MH_EHIP, to exercise the hand-back path on a one-GPU box
     int fail_worker = -1;
+    // MINEHIP_TEST_SPAWN_LIMIT=k (dev build only): the host thread of every worker after the first
+    // k fails to start (std::system_error, as when the process is out of threads), so the
+    // start-failure path of both coordinators runs on any box
+    mh::ThreadStart start;
 #ifdef MH_DEV_HOOKS
     if (const char* e = getenv("MINEHIP_TEST_FAIL_WORKER")) fail_worker = atoi(e);
+    if (const char* e = getenv("MINEHIP_TEST_SPAWN_LIMIT")) {
+        auto started = std::make_shared<std::atomic<int>>(0);
+        const int limit = atoi(e);
+        start = [started, limit](std::function<void()> fn) {
+            if ((*started)++ >= limit)
+                throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again));
+            return std::thread(std::move(fn));
+        };
+    }
 #endif
-    if (ndev == 1 && chunk == 0 && fail_worker < 0)
+    if (ndev == 1 && chunk == 0 && fail_worker < 0 && !start)
         return search_impl(devs[0], pre, lower, upper, out_hash, out_nonce);
     // Adaptive: one rate-weighted shard per device (+ a short dynamic tail on long ranges), multi.hpp.
     if (chunk == 0) {
@@ -444,90 +475,23 @@ int mh_search_multi(const int* devs, int ndev, const uint8_t* msg, size_t len, u
             return r;
         };
         std::string err;
-        const int r = mh::search_shards(devs, ndev, pre, lower, upper, plan_opts(), search, out_hash, out_nonce, &err);
+        const int r = mh::search_shards(devs, ndev, pre, lower, upper, plan_opts(), search, out_hash, out_nonce, &err,
+                                        start);
         return r ? fail(r, err) : MH_OK;
     }
     // Fixed chunks: one miner per listed device, fed by the server's scheduler (sched.hpp) with
-    // chunks of exactly `chunk` nonces.  A device that fails hands its chunk back to the others.
-    mh_sched_opts o;
-    mh_sched_default_opts(&o);
-    o.init_chunk = o.min_chunk = o.max_chunk = chunk;
-    mh::Scheduler sched(o);
-    for (int i = 0; i < ndev; ++i) sched.add_miner(i);
-    if (sched.submit(0, msg, len, lower, upper) < 0) return fail(MH_EINTERNAL, "internal: submit failed");
-    std::mutex mu;
-    std::condition_variable cv;
-    uint64_t gen = 0;  // bumped on every completion or device loss
-    int alive = ndev, first_err = 0;
-    bool done = false;
-    mh_completion res{};
-    std::string err_msg;
-    auto now = []() { return now_ns(); };
-    std::vector<std::thread> th;
-    auto miner = [&](int i) {
-        for (;;) {
-            uint64_t seen;
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                if (done) return;
-                seen = gen;
-            }
-            mh_assignment a;
-            if (sched.next(i, now(), &a) != 1) {
-                // nothing to hand out: wait for the job to finish, or for a
-                // failed device's chunk to come back
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return done || gen != seen; });
-                continue;
-            }
-            uint64_t h, nn;
-            const int r = (i == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
-                                             : search_impl(devs[i], pre, a.lower, a.upper, &h, &nn);
-            if (r) {
-                const std::string e = g_err;
-                sched.remove_miner(i);  // its chunk goes back to the job
-                std::lock_guard<std::mutex> lk(mu);
-                if (!first_err) {
-                    first_err = r;
-                    err_msg = e;
-                }
-                if (--alive == 0) done = true;
-                ++gen;
-                cv.notify_all();
-                return;
-            }
-            mh_completion c;
-            const int q = sched.result(i, h, nn, now(), &c);
-            std::lock_guard<std::mutex> lk(mu);
-            if (q == 1) {
-                res = c;
-                done = true;
-            }
-            ++gen;
-            cv.notify_all();
-        }
+    // chunks of exactly `chunk` nonces (multi.cpp search_chunks).  A device that fails hands its
+    // chunk back to the others.
+    const mh::ChunkSearch csearch = [&](int worker, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* nn,
+                                        std::string* err) {
+        const int r = (worker == fail_worker) ? fail(MH_EHIP, "injected failure (dev build test hook)")
+                                              : search_impl(devs[worker], pre, lo, hi, h, nn);
+        if (r) *err = g_err;
+        return r;
     };
-    try {
-        for (int i = 0; i < ndev; ++i) th.emplace_back(miner, i);
-    } catch (...) {
-        // out of threads: the miners that did not start leave the scheduler (their chunks, if
-        // any, go back to the job) and the started ones finish the job
-        for (size_t i = th.size(); i < (size_t)ndev; ++i) sched.remove_miner((int64_t)i);
-        std::lock_guard<std::mutex> lk(mu);
-        alive -= ndev - (int)th.size();
-        if (!first_err) {
-            first_err = MH_EINTERNAL;
-            err_msg = "could not start a host thread per device";
-        }
-        if (alive == 0) done = true;
-        ++gen;
-        cv.notify_all();
-    }
-    for (auto& t : th) t.join();
-    if (alive == 0) return fail(first_err ? first_err : MH_EHIP, err_msg.empty() ? "every device failed" : err_msg);
-    *out_hash = res.hash;
-    *out_nonce = res.nonce;
-    return MH_OK;
+    std::string err;
+    const int r = mh::search_chunks(ndev, msg, len, lower, upper, chunk, csearch, out_hash, out_nonce, &err, start);
+    return r ? fail(r, err) : MH_OK;
 }
 
 int mh_hash_batch(int dev, const uint8_t* msg, size_t len, const uint64_t* nonces, size_t n, uint64_t* out_hashes) {

@@ -2,12 +2,14 @@
 #include "multi.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
 #include <thread>
 
 #include "../../include/minehip.h"
+#include "sched.hpp"
 
 namespace mh {
 namespace {
@@ -26,6 +28,10 @@ std::vector<Span> split_even(const Span& s, int parts) {
         prev = pos;
     }
     return out;
+}
+
+std::thread start_thread(const ThreadStart& start, std::function<void()> fn) {
+    return start ? start(std::move(fn)) : std::thread(std::move(fn));
 }
 
 }  // namespace
@@ -90,7 +96,7 @@ void multi_plan(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOpt
 
 int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, uint64_t upper,
                   const PlanOpts& opt, const SpanSearch& search, uint64_t* out_hash, uint64_t* out_nonce,
-                  std::string* err) {
+                  std::string* err, const ThreadStart& start) {
     MultiPlan mp;
     multi_plan(pre, lower, upper, opt, worker_weights(devs, ndev), &mp);
     std::mutex mu;
@@ -147,7 +153,7 @@ int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, 
     };
     std::vector<std::thread> th;
     try {
-        for (int i = 0; i < ndev; ++i) th.emplace_back(worker, i);
+        for (int i = 0; i < ndev; ++i) th.push_back(start_thread(start, [&worker, i] { worker(i); }));
     } catch (...) {
         // out of threads: the workers that started take the heads of those that did not
         std::lock_guard<std::mutex> lk(mu);
@@ -170,6 +176,97 @@ int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, 
     }
     *out_hash = bh;
     *out_nonce = bn;
+    return MH_OK;
+}
+
+int search_chunks(int ndev, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, uint64_t chunk,
+                  const ChunkSearch& search, uint64_t* out_hash, uint64_t* out_nonce, std::string* err,
+                  const ThreadStart& start) {
+    mh_sched_opts o;
+    mh_sched_default_opts(&o);
+    o.init_chunk = o.min_chunk = o.max_chunk = chunk;
+    Scheduler sched(o);
+    for (int i = 0; i < ndev; ++i) sched.add_miner(i);
+    if (sched.submit(0, msg, len, lower, upper) < 0) {
+        *err = "internal: submit failed";
+        return MH_EINTERNAL;
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;  // bumped on every completion or worker loss
+    int alive = ndev, first_err = 0;
+    bool done = false;
+    mh_completion res{};
+    std::string err_msg;
+    auto now = []() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
+    auto miner = [&](int i) {
+        for (;;) {
+            uint64_t seen;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (done) return;
+                seen = gen;
+            }
+            mh_assignment a;
+            if (sched.next(i, now(), &a) != 1) {
+                // nothing to hand out: wait for the job to finish, or for a failed worker's chunk
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return done || gen != seen; });
+                continue;
+            }
+            uint64_t h = 0, nn = 0;
+            std::string e;
+            const int r = search(i, a.lower, a.upper, &h, &nn, &e);
+            if (r) {
+                sched.remove_miner(i);  // its chunk goes back to the job
+                std::lock_guard<std::mutex> lk(mu);
+                if (!first_err) {
+                    first_err = r;
+                    err_msg = e;
+                }
+                if (--alive == 0) done = true;
+                ++gen;
+                cv.notify_all();
+                return;
+            }
+            mh_completion c;
+            const int q = sched.result(i, h, nn, now(), &c);
+            std::lock_guard<std::mutex> lk(mu);
+            if (q == 1) {
+                res = c;
+                done = true;
+            }
+            ++gen;
+            cv.notify_all();
+        }
+    };
+    std::vector<std::thread> th;
+    try {
+        for (int i = 0; i < ndev; ++i) th.push_back(start_thread(start, [&miner, i] { miner(i); }));
+    } catch (...) {
+        // out of threads: the miners that did not start leave the scheduler (their chunks, if
+        // any, go back to the job) and the started ones finish the job
+        for (size_t i = th.size(); i < (size_t)ndev; ++i) sched.remove_miner((int64_t)i);
+        std::lock_guard<std::mutex> lk(mu);
+        alive -= ndev - (int)th.size();
+        if (!first_err) {
+            first_err = MH_EINTERNAL;
+            err_msg = "could not start a host thread per device";
+        }
+        if (alive == 0) done = true;
+        ++gen;
+        cv.notify_all();
+    }
+    for (auto& t : th) t.join();
+    if (alive == 0) {
+        *err = err_msg.empty() ? "every device failed" : err_msg;
+        return first_err ? first_err : MH_EHIP;
+    }
+    *out_hash = res.hash;
+    *out_nonce = res.nonce;
     return MH_OK;
 }
 

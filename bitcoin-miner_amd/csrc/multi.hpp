@@ -16,6 +16,7 @@
 
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "plan.hpp"
@@ -47,10 +48,29 @@ double device_rate(int dev);
 using SpanSearch = std::function<int(int worker, int dev, uint64_t lo, uint64_t hi, uint64_t* hash,
                                      uint64_t* nonce, uint64_t* busy_ns, std::string* err)>;
 
+// Starts one worker's host thread (std::thread by default).  May throw, as std::thread's
+// constructor does when the process is out of threads; the dev build's MINEHIP_TEST_SPAWN_LIMIT
+// and tests/host/tsan_multi.cpp inject a starter that throws after k threads.
+using ThreadStart = std::function<std::thread(std::function<void()>)>;
+
 // Runs the split with one host thread per worker.  MH_OK with the lexicographic minimum, or the
-// first failure's code and text when every worker failed (some span was left unsearched).
+// first failure's code and text when every worker failed (some span was left unsearched).  Workers
+// whose thread could not start leave their heads to the others.
 int search_shards(const int* devs, int ndev, const Prefix& pre, uint64_t lower, uint64_t upper,
                   const PlanOpts& opt, const SpanSearch& search, uint64_t* out_hash, uint64_t* out_nonce,
-                  std::string* err);
+                  std::string* err, const ThreadStart& start = {});
+
+// One search of [lo, hi] by `worker` (the fixed-chunk path): the (hash, nonce) minimum, or an MH_E*
+// code with *err describing it.
+using ChunkSearch = std::function<int(int worker, uint64_t lo, uint64_t hi, uint64_t* hash, uint64_t* nonce,
+                                      std::string* err)>;
+
+// mh_search_multi with chunk > 0: one miner per worker, fed by the server's scheduler (sched.hpp)
+// with chunks of exactly `chunk` nonces, one host thread each; a worker that fails hands its chunk
+// back to the others, and so do workers whose thread could not start.  MH_OK with the minimum, or
+// the first failure's code and text when no worker was left.
+int search_chunks(int ndev, const uint8_t* msg, size_t len, uint64_t lower, uint64_t upper, uint64_t chunk,
+                  const ChunkSearch& search, uint64_t* out_hash, uint64_t* out_nonce, std::string* err,
+                  const ThreadStart& start = {});
 
 }  // namespace mh

@@ -165,18 +165,8 @@ uint32_t nonce_ops(int J, int mode) { return nonce_cost(J, mode).ops; }
 
 namespace {
 
-// The instantiated fast kernels (fast_search.hip; search_kernels.hip fast_variant_exists).
-bool kernel_exists(int J, int mode) {
-    switch (mode) {
-        case kModeOne: return J >= 0 && J <= 13;
-        case kModePre: return J >= 0 && J <= 4;
-        case kModeTwo: return J >= 13 && J <= 15;
-        case kModeOneEarly: return J == 0 || J == 8;
-        case kModePreEarly: return J == 0;
-        case kModeTwoEarly: return J == 13;
-        default: return false;
-    }
-}
+// The instantiated fast kernels (layout.hpp MH_FAST_KERNELS, the launcher's list too).
+bool kernel_exists(int J, int mode) { return fast_kernel_exists(J, mode); }
 
 // Fast-kernel launch template for bucket d with L lower digits.  early: the digit ending the word
 // before the last digit's is enumerated innermost (layout.hpp kMode*Early) -- false when the
@@ -279,8 +269,12 @@ bool pick_layout(const Prefix& pre, int d, int L, uint64_t A, uint64_t B, const 
         int Je, me, nbe;
         uint64_t be;
         FastArgs fe;
+        // a launch holds whole blocks (emit_runs), so an Early block must fit the launch caps: the
+        // caps are then kept exactly, rounded up only to one 10^L-nonce lane
+        const uint64_t max_gen = (uint64_t)std::min(opt.max_blocks, kMaxBlocksPerLaunch) * kBlockThreads;
         if (make_fast_args(pre, d, L, true, &Je, &me, &nbe, &be, &fe) &&
-            nonce_cost(Je, me).slots < nonce_cost(*J, *mode).slots && B - A >= 2u * be) {
+            nonce_cost(Je, me).slots < nonce_cost(*J, *mode).slots && B - A >= 2u * be &&
+            be <= opt.max_nonces_per_launch && be / kPow10[L] <= max_gen) {
             *J = Je;
             *mode = me;
             *nb = nbe;
@@ -458,7 +452,9 @@ void plan_search(const Prefix& pre, uint64_t lower, uint64_t upper, const PlanOp
         const unsigned __int128 Rx = kPow10[Lx];
         const uint64_t lpb = Bx / (uint64_t)Rx;  // lanes per block
         uint64_t max_runs = std::min<uint64_t>(max_gen, opt.max_nonces_per_launch / (uint64_t)Rx);
-        max_runs = std::max<uint64_t>(lpb, max_runs / lpb * lpb);  // whole blocks per launch
+        // whole blocks per launch; pick_layout takes an Early layout (lpb > 1) only when one block
+        // fits the caps, so this rounds up only a cap below one 10^L-nonce lane
+        max_runs = std::max<uint64_t>(lpb, max_runs / lpb * lpb);
         ua *= lpb;
         ub *= lpb;
         for (unsigned __int128 u = ua; u < ub;) {

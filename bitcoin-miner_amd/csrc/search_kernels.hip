@@ -203,17 +203,7 @@ hipError_t fast_function(int dev, int J, int mode, hipFunction_t* f, bool* queue
     return hipSuccess;
 }
 
-bool fast_variant_exists(int J, int mode) {
-    switch (mode) {
-        case kModeOne: return J >= 0 && J <= 13;
-        case kModePre: return J >= 0 && J <= 4;   // last digit at tail byte 64..82 (t <= 63, d <= 20)
-        case kModeTwo: return J >= 13 && J <= 15;
-        case kModeOneEarly: return J == 0 || J == 8;  // fast_search.hip's Early instantiations
-        case kModePreEarly: return J == 0;
-        case kModeTwoEarly: return J == 13;
-        default: return false;
-    }
-}
+bool fast_variant_exists(int J, int mode) { return fast_kernel_exists(J, mode); }  // layout.hpp MH_FAST_KERNELS
 }  // namespace
 
 // Load the fast_search module on dev (the current device) at context setup,

@@ -129,6 +129,8 @@ static void fuzz_plan() {
     o.lower_digits = 1 + (int)rnd(5);
     o.min_lanes = rnd(2) ? 1 : (1ull << rnd(20));
     o.max_nonces_per_launch = 1ull + rnd(1ull << 33);
+    if (rnd(2)) o.max_blocks = 1u + (uint32_t)rnd(1u << 17);
+    const uint64_t max_gen = (uint64_t)std::min(o.max_blocks, mh::kMaxBlocksPerLaunch) * mh::kBlockThreads;
     o.generic_below = rnd(2) ? 0 : rnd(1ull << 21);
     o.early = (int)rnd(2);
     o.fine_tail = rnd(2) ? 0 : rnd(1ull << 29);
@@ -142,8 +144,10 @@ static void fuzz_plan() {
         }
         if (p.kind == 0) {
             const uint64_t R = kP10[p.L];
+            // the launch caps hold, rounded up to one lane at most (an Early block always fits them)
             if (p.L < 1 || p.L > 5 || p.first % R || p.count % R || p.fa.n_runs == 0 ||
                 (uint64_t)p.fa.n_runs * R != p.count || p.fa.n_hi + p.fa.L > 20 ||
+                p.count > std::max<uint64_t>(o.max_nonces_per_launch, R) || p.fa.n_runs > max_gen ||
                 !lanes_format_their_nonces(pre, p)) {
                 bad = true;
                 return false;

@@ -21,15 +21,22 @@
 #include <cmath>
 #include <atomic>
 #include <chrono>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <set>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
 #include "../../bitcoin-miner_amd/csrc/multi.hpp"
 #include "../../include/minehip.h"
+
+namespace mh {
+int set_error(int code, const char*) { return code; }  // the scheduler's error slot (minehip.cpp's is per thread)
+}  // namespace mh
 
 static int g_fail = 0;
 #define CHECK(c)                                                                  \
@@ -120,6 +127,83 @@ static void one_case(std::mt19937_64& rng, int it) {
         }
 }
 
+// A starter whose threads after the first k fail to start (as std::thread does when the process
+// is out of threads): MINEHIP_TEST_SPAWN_LIMIT's stand-in.
+static mh::ThreadStart limited(int k) {
+    auto n = std::make_shared<std::atomic<int>>(0);
+    return [n, k](std::function<void()> fn) {
+        if ((*n)++ >= k) throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again));
+        return std::thread(std::move(fn));
+    };
+}
+
+// Both coordinators (rate-weighted shards, fixed scheduler chunks) with only k of ndev host threads
+// started: with k > 0 the started workers take the others' work and the job ends with the minimum
+// over spans that tile the range once; with k = 0 the call fails with MH_EINTERNAL.
+static void spawn_failures(std::mt19937_64& rng) {
+    for (int ndev : {1, 2, 5, 8}) {
+        for (int k : {0, 1, ndev - 1, ndev}) {
+            if (k < 0 || (k == ndev - 1 && ndev == 1)) continue;
+            for (int path = 0; path < 2; ++path) {
+                const uint64_t lower = rng() % (1ull << 40);
+                const uint64_t upper = lower + (rng() % 4 + 1) * ((uint64_t)ndev << 34);
+                std::mutex mu;
+                std::vector<Rec> done;
+                std::set<int> workers;
+                auto rec = [&](int worker, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* n) {
+                    std::this_thread::sleep_for(std::chrono::microseconds(splitmix(lo) % 200));
+                    *h = splitmix(lo * 31 + hi);
+                    *n = lo + splitmix(hi) % (hi - lo + 1);
+                    std::lock_guard<std::mutex> lk(mu);
+                    done.push_back(Rec{lo, hi, *h, *n});
+                    workers.insert(worker);
+                };
+                std::vector<int> devs((size_t)ndev, 20);  // device 20: a rate of its own, unused elsewhere
+                uint64_t oh = 0, on = 0;
+                std::string err;
+                int rc;
+                if (path == 0) {
+                    mh::Prefix pre;
+                    mh::absorb_prefix((const uint8_t*)"cmu440", 6, &pre);
+                    const mh::SpanSearch s = [&](int w, int, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* n,
+                                                 uint64_t* ns, std::string*) {
+                        rec(w, lo, hi, h, n);
+                        *ns = 1 + (hi - lo) / 50;
+                        return MH_OK;
+                    };
+                    rc = mh::search_shards(devs.data(), ndev, pre, lower, upper, mh::PlanOpts(), s, &oh, &on, &err,
+                                           limited(k));
+                } else {
+                    const mh::ChunkSearch s = [&](int w, uint64_t lo, uint64_t hi, uint64_t* h, uint64_t* n,
+                                                  std::string*) {
+                        rec(w, lo, hi, h, n);
+                        return MH_OK;
+                    };
+                    const uint64_t chunk = (upper - lower) / 40 + 1;
+                    rc = mh::search_chunks(ndev, (const uint8_t*)"cmu440", 6, lower, upper, chunk, s, &oh, &on, &err,
+                                           limited(k));
+                }
+                if (k == 0) {
+                    CHECK(rc == MH_EINTERNAL && err.find("could not start") != std::string::npos && done.empty());
+                    continue;
+                }
+                CHECK(rc == MH_OK);
+                CHECK(*workers.rbegin() < k);  // only started workers searched
+                std::sort(done.begin(), done.end(), [](const Rec& a, const Rec& b) { return a.lo < b.lo; });
+                CHECK(!done.empty() && done.front().lo == lower && done.back().hi == upper);
+                for (size_t i = 1; i < done.size(); ++i) CHECK(done[i - 1].hi + 1 == done[i].lo);
+                uint64_t bh = ~0ull, bn = ~0ull;
+                for (const auto& r : done)
+                    if (r.h < bh || (r.h == bh && r.n < bn)) {
+                        bh = r.h;
+                        bn = r.n;
+                    }
+                CHECK(oh == bh && on == bn);
+            }
+        }
+    }
+}
+
 // A device listed k times runs its k shards one after another, so each of its entries weighs 1/k of
 // its rate and every physical device carries a share of the range in proportion to its own rate
 // (devices 10..12: never listed by one_case, so their rates are only these).
@@ -149,6 +233,7 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 100;
     std::mt19937_64 rng(seed);
     repeated_devices();
+    spawn_failures(rng);
     for (int it = 0; it < iters; ++it) one_case(rng, it);
     printf("iterations=%d failures=%d\n", iters, g_fail);
     return g_fail ? 1 : 0;

@@ -349,6 +349,27 @@ def test_every_instantiated_kernel_is_reachable():
     assert set(kernel_cases()) == KERNELS
 
 
+def test_one_kernel_list():
+    """layout.hpp's MH_FAST_KERNELS is the one list of fast_search layouts: the kernels
+    fast_search.hip instantiates and the planner and the launcher accept (both call
+    fast_kernel_exists over it), and the per-nonce loops csrc/loop_mix.py expects.  It is the set
+    this file expects, and the embedded code object holds exactly its kernels."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd", "csrc"))
+    import loop_mix
+    assert loop_mix.fast_kernels() == KERNELS
+    from minehip import codeobj
+    names = {k[".name"] for k in codeobj.metadata(codeobj.fast_code_object())["amdhsa.kernels"]}
+    got = {tuple(int(x) for x in re.match(r"_ZN2mh11fast_searchILi(\d+)ELi(\d+)EE", n).groups())
+           for n in names if "fast_search" in n}
+    assert got == KERNELS
+    src = {f: open(os.path.join(ROOT, "bitcoin-miner_amd", "csrc", f)).read()
+           for f in ("plan.cpp", "search_kernels.hip", "fast_search.hip")}
+    assert "return fast_kernel_exists(J, mode);" in src["plan.cpp"]
+    assert "return fast_kernel_exists(J, mode);" in src["search_kernels.hip"]
+    assert "MH_FAST_KERNELS(MH_INST)" in src["fast_search.hip"]
+
+
 def test_embedded_code_object_carries_queue_marker():
     """The work queue is used only with a code object that carries fast_search.hip's
     mh_fast_queue_args marker at sizeof(FastArgs): the embedded object does, at the

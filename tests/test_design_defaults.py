@@ -66,3 +66,20 @@ def test_integration_knobs_match_the_library():
     for env, default in knobs.items():
         assert env in field_of, env
         assert _num(default) == _num(code[field_of[env]]), (env, default, code[field_of[env]])
+
+
+def test_launch_size_statement():
+    """DESIGN.md §3 states the launch size as a departure from SURVEY §8(b) B3's "<= 100 ms" bound
+    (VERDICT r05 item 4): the longest launch it names is PlanOpts' caps, min(max_nonces_per_launch,
+    max_blocks x 256 lanes x 10^lower_digits) nonces, and the milliseconds it gives are that many
+    nonces at the GH/s it cites."""
+    code = plan_defaults()
+    longest = min(_num(code["max_nonces_per_launch"]), _num(code["max_blocks"]) * 256 * 10 ** int(code["lower_digits"]))
+    doc = open(os.path.join(ROOT, "DESIGN.md")).read()
+    sec = doc[doc.index("**Launch size: a deliberate departure from SURVEY §8(b) B3.**"):]
+    sec = sec[:sec.index("\n\n")]
+    n = int(re.search(r"\*\*([\d,]+) nonces\*\*", sec).group(1).replace(",", ""))
+    assert n == longest
+    ms = int(re.search(r"\*\*about (\d+) ms\*\*", sec).group(1))
+    ghs = float(re.search(r"at the\s+driver's ([\d.]+) GH/s", sec).group(1))
+    assert abs(ms - n / ghs / 1e6) < 10, (ms, n / ghs / 1e6)

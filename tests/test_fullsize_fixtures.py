@@ -9,7 +9,7 @@ import os
 
 import pytest
 
-from conftest import load_golden
+from conftest import GOLDEN, load_golden
 from oracle import oracle
 
 CFGS = {"cfg2": (b"cmu440", (1 << 35) - 1), "cfg3a": (b"a" * 100, (1 << 34) - 1),
@@ -54,6 +54,30 @@ def test_fixture_chunk_vs_oracle(name):
     i = {"cfg2": 255, "cfg3a": 611, "cfg3b": 1000, "cfg5c": 15}.get(name, 255)  # cfg*: d = 10, 11, 11; the rest: last
     got = oracle.search(msg, lo + i * size, lo + (i + 1) * size - 1, threads=os.cpu_count() or 1)
     assert got == tuple(d["chunks"][i])
+
+
+def test_config5_sample_fixture():
+    """fullsize_cfg5s.json: 64 2^28-nonce chunks spread over [2^40, 2^42), the
+    range's first and last chunk among them, as gen_cfg5s.sample_los() draws them; every minimum
+    re-hashes through the oracle and lies in its chunk; one chunk is rescanned by the oracle; the
+    answer chunk's minimum (configs[4]'s answer, fullsize_cfg5c.json) beats every sample."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import gen_cfg5s
+    d = load_golden("fullsize_cfg5s.json")
+    assert bytes.fromhex(d["msg_hex"]) == b"cmu440" and (d["lo"], d["hi"]) == (1 << 40, (1 << 42) - 1)
+    los = [s[0] for s in d["samples"]]
+    assert los == gen_cfg5s.sample_los() and len(los) == 64
+    assert los[0] == 1 << 40 and d["samples"][-1][1] == (1 << 42) - 1
+    stride = 3 << 34
+    assert all((los[i] - (1 << 40)) // stride == i for i in range(64))  # one per 3 * 2^34 stride
+    for lo, hi, h, n in d["samples"]:
+        assert hi - lo + 1 == 1 << d["chunk_bits"] == 1 << 28 and lo <= n <= hi
+        assert oracle.hash_(b"cmu440", n) == h
+    lo, hi, h, n = d["samples"][0]
+    assert oracle.search(b"cmu440", lo, hi, threads=os.cpu_count() or 1) == (h, n)
+    answer = tuple(load_golden("fullsize_cfg5c.json")["result"])
+    assert all(answer < (h, n) for _, _, h, n in d["samples"])
 
 
 def test_sample_fixture():

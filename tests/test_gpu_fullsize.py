@@ -27,6 +27,7 @@ reproduce every one of them:
   cfg4s  "cmu440": 100 chunks sampled from configs[3]/[4] ([0, 2^42-1], d = 11..13)
   cfg4   "cmu440" [0, 2^40-1]: configs[3] whole, its 256 2^32-chunk minima
          (tests/golden/gen_cfg4.py: SHA-NI scan, checked against OpenSSL)
+  cfg5s  "cmu440": 64 sampled 2^28 chunks of [2^40, 2^42-1] (tests/golden/gen_cfg5s.py, SHA-NI)
   cfg5c  "cmu440" [1017 * 2^32, 1018 * 2^32 - 1]: the 2^32 chunk of configs[4] that holds its
          answer, in 2^28 chunks (tests/golden/gen_cfg5c.py: SHA-NI scan, checked against OpenSSL);
          configs[4] itself runs in test_e2e_cluster.py (direct and over LSP with 8 miners)
@@ -105,6 +106,20 @@ def test_config4_5_samples(gpu):
     msg = bytes.fromhex(d["msg_hex"])
     bad = [(lo, hi) for lo, hi, h, n in d["samples"] if gpu.search(msg, lo, hi) != (h, n)]
     assert not bad, bad[:3]
+
+
+def test_config5_sampled_chunks(gpu):
+    """BASELINE configs[4] ([0, 2^42-1]) above configs[3]: [2^40, 2^42) is pinned on the CPU by 64
+    sampled 2^28-nonce chunks (tests/golden/gen_cfg5s.py: SHA-NI, one chunk rescanned with OpenSSL;
+    VERDICT r05 item 3).  Every chunk searched on the GPU gives its CPU minimum, and the answer
+    chunk's minimum (fullsize_cfg5c.json: configs[4]'s answer) beats every sample."""
+    d = load_golden("fullsize_cfg5s.json")
+    msg = bytes.fromhex(d["msg_hex"])
+    assert (d["lo"], d["hi"]) == (1 << 40, (1 << 42) - 1) and len(d["samples"]) >= 64
+    bad = [(lo, hi) for lo, hi, h, n in d["samples"] if gpu.search(msg, lo, hi) != (h, n)]
+    assert not bad, bad[:3]
+    answer = tuple(load_golden("fullsize_cfg5c.json")["result"])
+    assert all(answer < (h, n) for _, _, h, n in d["samples"])
 
 
 def test_plan_knobs_full_size(gpu):

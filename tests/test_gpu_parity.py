@@ -124,11 +124,11 @@ def test_every_kernel_instantiation(gpu):
                 assert gpu.search(m, lo, hi) == exp, (J, mode, len(m), Ld)
 
 
-def early_position_cases(Ls=(1, 2, 3)):
+def early_position_cases(Ls=(1, 2, 3), max_p=4):
     """(msg, lo, hi, L, J, mode, p) for every (Early kernel, innermost position p, L) the planner
     can produce: messages of every tail offset, each bucket d = 2..20 from its first nonce (and
-    the top of the u64 range for d = 20), two blocks of lanes (10^(p+L) nonces each) plus a
-    ragged edge.  Host only."""
+    the top of the u64 range for d = 20), two blocks of lanes (10^(p+L) nonces each, p <= max_p)
+    plus a ragged edge.  Host only."""
     import minehip
     cases = {}
     for n in range(0, 128):
@@ -137,7 +137,7 @@ def early_position_cases(Ls=(1, 2, 3)):
         for d in range(2, 21):
             for Ld in Ls:
                 with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
-                    size = 2 * 10 ** (4 + Ld) + 3_456  # two blocks at p = 4
+                    size = 2 * 10 ** (max_p + Ld) + 3_456  # two blocks at p = max_p
                     los = [10 ** (d - 1)] + ([U64 - size] if d == 20 else [])
                     for lo in los:
                         hi = min(U64, lo + size)
@@ -162,7 +162,14 @@ def test_early_layout_every_position(gpu):
     kinds = {(J, mode) for (J, mode, *_rest) in cases}
     assert kinds == {(0, 3), (8, 3), (0, 4), (13, 5)}, kinds
     assert any(p < L for (_, _, p, L, _) in cases) and any(p >= L for (_, _, p, L, _) in cases)
-    for key, (m, lo, hi, Ld) in sorted(cases.items()):
+    # L = 4 (MINEHIP_LOWER_DIGITS >= 4): the whole of word J enumerated, the group three digits;
+    # at p = 1 (two blocks are 2 x 10^5 nonces, oracle-sized), one case per Early kernel that
+    # plans at L = 4.  <0, OneEarly> never does: word 0 all digits puts the first
+    # digit at byte 0, so p = d - 4 and a block of 10^(p+4) = 10^d nonces exceeds its bucket
+    cases4 = early_position_cases(Ls=(4,), max_p=1)
+    assert {(J, mode) for (J, mode, *_rest) in cases4} == kinds - {(0, 3)}, cases4.keys()
+    assert all(p == 1 and L == 4 for (_, _, p, L, _) in cases4)
+    for key, (m, lo, hi, Ld) in sorted(cases.items()) + sorted(cases4.items()):
         exp = oracle.search(m, lo, hi, threads=8)
         with env(MINEHIP_LOWER_DIGITS=Ld, MINEHIP_MIN_LANES=1, MINEHIP_GENERIC_BELOW=0):
             assert gpu.search(m, lo, hi) == exp, (key, len(m), lo, hi)

@@ -94,16 +94,18 @@ def test_scheduler_under_thread_sanitizer(tmp_path):
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
 def test_multi_coordinator_under_sanitizers(tmp_path, san):
     """mh_search_multi's shard coordinator (csrc/multi.cpp: rate-weighted head shards, dynamic tail,
-    hand-back of a failed worker's span) from up to 8 worker threads with a stand-in search that
-    fails for random workers (tests/host/tsan_multi.cpp): the successful spans tile the range once,
-    the merge is the minimum over them, and the call fails exactly when every worker failed."""
+    hand-back of a failed worker's span) and the fixed-chunk scheduler path (search_chunks) from up
+    to 8 worker threads with a stand-in search that fails for random workers, and with only k of
+    the workers' host threads started (tests/host/tsan_multi.cpp): the successful spans tile the
+    range once, the merge is the minimum over them, and the call fails exactly when every worker
+    failed or none started (MH_EINTERNAL)."""
     if shutil.which("g++") is None:
         pytest.skip("no g++")
     out = str(tmp_path / "tsan_multi")
     extra = ["-fno-sanitize-recover=undefined"] if "undefined" in san else []
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={san}", *extra, "-Wall",
            "-o", out, os.path.join(ROOT, "tests", "host", "tsan_multi.cpp"), os.path.join(CSRC, "multi.cpp"),
-           os.path.join(CSRC, "plan.cpp"), "-lpthread"]
+           os.path.join(CSRC, "plan.cpp"), os.path.join(CSRC, "sched.cpp"), "-lpthread"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",

@@ -12,7 +12,8 @@ Recipe (JSON):
   {"about": "...", "tag": "r03u",
    "variants": {"name": "K=V,K=V" | "", ...},          # "" = the product build as is
    "code_objects": {"name": "build/ab/x.hsaco"},       # shorthand: MINEHIP_DEV_CODE_OBJECT=...
-   "workloads": [["d10", 7, "clock"], ["cfg1", 9], ...],  # WORKLOADS name, rounds, optional clock
+   "workloads": [["d10", 7, "clock"], ["cfg1", 9], ...],  # WORKLOADS name, rounds, optional clock,
+                                                          # optional "energy<R>" (R energy windows)
    "retired": "why"}   # optional: the knobs it varies left the library; kept as the record, not run
 The recipes under tools/ab/ are the experiments behind DESIGN.md and profiles/ (HISTORY.md).
 """
@@ -87,10 +88,38 @@ def commands(recipe, variants, only=None):
                 "--count", str(count), "--rounds", str(rounds)]
         if "clock" in w[2:]:
             argv.append("--clock")
+        for opt in w[2:]:  # "energy<R>": R interleaved clock + energy windows per variant (kbench --energy)
+            if isinstance(opt, str) and opt.startswith("energy"):
+                argv += ["--energy", opt[len("energy"):] or "3"]
         for v, env in variants.items():
             argv += ["--var", f"{v}:{env}"]
         out.append((name, argv))
     return out
+
+
+def ensure_code_objects(recipe):
+    """Build the recipe's missing code objects where the run happens (the
+    variants are not pushed to every GPU box): build/isa/<v>.hsaco by tools/isa_variant.py <v>,
+    build/ab/<v>.hsaco by tools/co_variants.py <v> (from the compiler's build/fast_search.s)."""
+    for name, co in recipe.get("code_objects", {}).items():
+        path = os.path.join(ROOT, co)
+        if os.path.exists(path):
+            continue
+        d, v = os.path.dirname(co), os.path.basename(co)[:-len(".hsaco")]
+        if d == "build/isa":
+            cmd = [sys.executable, os.path.join(ROOT, "tools", "isa_variant.py"), v]
+        elif d == "build/ab":
+            s = os.path.join(ROOT, "build", "fast_search.s")
+            if not os.path.exists(s):
+                subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                                "--cuda-device-only", "-S", "-o", s,
+                                os.path.join(ROOT, "bitcoin-miner_amd", "csrc", "fast_search.hip")], check=True)
+            cmd = [sys.executable, os.path.join(ROOT, "tools", "co_variants.py"), v]
+        else:
+            raise SystemExit(f"code object {co} ({name}) is missing and has no builder")
+        print(f"building {co}: {' '.join(cmd[1:])}", flush=True)
+        if subprocess.run(cmd, cwd=ROOT).returncode != 0 or not os.path.exists(path):
+            raise SystemExit(f"could not build {co}")
 
 
 def main():
@@ -111,6 +140,7 @@ def main():
             print(name, " ".join(argv[1:]))
         return
     os.makedirs(out, exist_ok=True)
+    ensure_code_objects(recipe)
     for name, argv in cmds:
         with open(os.path.join(out, f"kbench_{name}.json"), "w") as fo, \
                 open(os.path.join(out, f"kbench_{name}.err"), "w") as fe:

@@ -213,6 +213,12 @@ for s in $STEPS; do
         rc=$?; echo "earlypmc $e rc=$rc" | tee -a "$OUT/session.log"; fatal $rc
       done
       ;;
+    energy)
+      # VALU instruction classes priced in joules at the power limit + the product's energy window
+      # (tools/energy_probe.py, build/libvaluenergy.so)
+      timeout -k 10 400 python "$ROOT/tools/energy_probe.py" --tag "$TAG" > "$OUT/energy_probe.log" 2>&1
+      rc=$?; echo "energy rc=$rc" | tee -a "$OUT/session.log"; tail -14 "$OUT/energy_probe.log"; fatal $rc
+      ;;
     ab:*)
       # an A/B recipe (tools/ab.py, tools/ab/<recipe>.json): one kbench process per workload
       recipe=${s#ab:}

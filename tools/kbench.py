@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--clock", action="store_true",
                     help="also read each variant's in-kernel clock during a 2^37-nonce search of "
                          "fast_search<4, One> (bench.kernel_clock; needs build/libclockprobe.so)")
+    ap.add_argument("--energy", type=int, default=0, metavar="R",
+                    help="R interleaved rounds of that clock search per variant, each also an energy "
+                         "window (tools/energy.py: J per 10^9 nonces, mean W, the active limit)")
     a = ap.parse_args()
     variants = []
     for v in a.var or ["base:"]:
@@ -70,6 +73,39 @@ def main():
                "wall_ghs_med": sorted(x["wall_ghs"] for x in v)[len(v) // 2],
                "wall_ghs_max": max(x["wall_ghs"] for x in v),
                "fast_ghs_max": max(x["fast_ghs"] for x in v), "result": v[-1]["result"]} for n, v in res.items()}
+    if a.energy:
+        sys.path[:0] = [ROOT, os.path.join(ROOT, "tools")]
+        import bench
+        import energy
+        meter = energy.meter_for_device(0)
+        runs = {n: [] for n, _ in variants}
+        for _ in range(a.energy):
+            for name, env in variants:
+                old = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
+                try:
+                    kc = bench.kernel_clock(lambda m, lo, hi: minehip.search(m, lo, hi), 0, meter=meter)
+                finally:
+                    for k, v in old.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
+                runs[name].append(kc or {})
+        for name, rs in runs.items():
+            def med(key, sub=None):
+                v = [(r.get(sub) or {}).get(key) if sub else r.get(key) for r in rs]
+                v = sorted(x for x in v if isinstance(x, (int, float)))
+                return v[len(v) // 2] if v else None
+            e = {"rounds": len(rs), "ghz_med": med("ghz"), "search_ghs_med": med("search_ghs"),
+                 "j_per_gnonce_med": med("j_per_gnonce", "energy"), "mean_w_med": med("mean_w", "energy"),
+                 "gfx_voltage_mv_med": med("gfx_voltage_mv", "energy"),
+                 "limiters": sorted({(r.get("energy") or {}).get("limiter") or "?" for r in rs}),
+                 "runs": [{"ghz": r.get("ghz"), "search_ghs": r.get("search_ghs"),
+                           "ghz_by_xcd": r.get("ghz_by_xcd"), "energy": r.get("energy")} for r in rs]}
+            if e["ghz_med"] and e["search_ghs_med"]:
+                e["simd_quads_per_64_nonces"] = round(e["ghz_med"] / e["search_ghs_med"] * 1024 * 64 / 4, 1)
+            out[name]["energy"] = e
     if a.clock:
         sys.path.insert(0, ROOT)
         import bench

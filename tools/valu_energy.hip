@@ -1,0 +1,136 @@
+// valu_energy.hip -- what one VALU instruction class costs in energy on gfx950 at the power limit
+// (price the instructions of the fast kernel's per-nonce loop in joules).
+//
+// Each kernel keeps every SIMD of the chip at 8 waves, each wave running ONE instruction class
+// (inline asm pins the encoding) over 8 independent register chains, 64 instructions per
+// iteration, until a fixed wall time has passed (s_memrealtime, 100 MHz), so every probe lasts as
+// long as the energy window around it whatever clock the chip holds.  Every wave records its
+// iterations, its shader cycles and 100 MHz ticks over the loop, and its XCD; the host (tools/
+// energy_probe.py) brackets the launch with the socket's energy counter and turns the counts into
+// wave-instructions per second and the clock the chip held.
+//
+// The operands toggle like the SHA-256 loop's: rotations of a running value, sums and three-way
+// xors with per-lane values.  Results go to a buffer of their own by vector stores (lane 0 of
+// each wave); nothing else is written.
+//
+// C-ABI (build/libvaluenergy.so, loaded with ctypes; measurement only):
+//   ve_kinds()                                        number of probe kinds
+//   ve_name(kind)                                     its name
+//   ve_valu_per_iter(kind), ve_salu_per_iter(kind)    instructions per wave-iteration
+//   ve_run(dev, kind, seconds, nwg, out)              launch nwg workgroups of 256 threads on
+//                                                     device dev and wait; out[4*w..4*w+3] =
+//                                                     {iterations, cycles, 100 MHz ticks, xcc} of
+//                                                     wave w (nwg*4 waves)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kXccIdReg = 20 | (3 << 11);  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4)
+
+#define CH8(A0, A1, A2, A3, A4, A5, A6, A7)                                                     \
+    asm volatile(A0 : "+v"(x0) : "v"(y), "v"(z));                                             \
+    asm volatile(A1 : "+v"(x1) : "v"(y), "v"(z));                                             \
+    asm volatile(A2 : "+v"(x2) : "v"(y), "v"(z));                                             \
+    asm volatile(A3 : "+v"(x3) : "v"(y), "v"(z));                                             \
+    asm volatile(A4 : "+v"(x4) : "v"(y), "v"(z));                                             \
+    asm volatile(A5 : "+v"(x5) : "v"(y), "v"(z));                                             \
+    asm volatile(A6 : "+v"(x6) : "v"(y), "v"(z));                                             \
+    asm volatile(A7 : "+v"(x7) : "v"(y), "v"(z));
+#define SAME8(A) CH8(A, A, A, A, A, A, A, A)
+#define X8(B) B B B B B B B B
+
+#define ALIGNBIT "v_alignbit_b32 %0, %0, %0, 7"
+#define ADD3 "v_add3_u32 %0, %1, %2, %0"
+#define BITOP3 "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96"
+#define ADD "v_add_u32_e32 %0, %1, %0"
+#define PRIO_H "s_setprio 3\n\t" ALIGNBIT
+#define PRIO_F "s_setprio 0\n\t" ADD
+#define PRIO_FB "s_setprio 0\n\t" BITOP3
+
+struct Kind {
+    const char* name;
+    int valu, salu;  // per wave-iteration (the loop's own compare and branch not counted)
+};
+constexpr Kind kKinds[] = {
+    {"sleep", 0, 1},           // waves resident, s_sleep only: the chip's floor with a kernel up
+    {"alignbit", 64, 0},       // half rate
+    {"add3", 64, 0},           // half rate
+    {"bitop3", 64, 0},         // full rate (xor3)
+    {"add", 64, 0},            // full rate
+    {"setprio", 0, 64},        // scalar: the issue-priority markers alone
+    {"h4f4_prio", 64, 16},     // 4 alignbit + 4 add with the product's markers (pairs issue)
+    {"h4b4_prio", 64, 16},     // 4 alignbit + 4 bitop3 with markers
+};
+constexpr int kNumKinds = sizeof(kKinds) / sizeof(kKinds[0]);
+
+template <int KIND>
+__global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, uint32_t s, uint64_t ticks) {
+    uint32_t x0 = (threadIdx.x * 0x9e3779b9u) ^ s, x1 = x0 * 3u + 1u, x2 = x0 * 5u + 7u, x3 = x0 * 7u + 11u,
+             x4 = x0 * 9u + 13u, x5 = x0 * 11u + 17u, x6 = x0 * 13u + 19u, x7 = x0 * 15u + 23u;
+    const uint32_t y = (threadIdx.x + s) * 0x85ebca6bu, z = (threadIdx.x ^ 0x5bd1e995u) * 0xc2b2ae35u;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t r = r0, it = 0;
+    while (r - r0 < ticks) {
+        if constexpr (KIND == 0) {
+            __builtin_amdgcn_s_sleep(8);
+        } else if constexpr (KIND == 1) {
+            X8(SAME8(ALIGNBIT))
+        } else if constexpr (KIND == 2) {
+            X8(SAME8(ADD3))
+        } else if constexpr (KIND == 3) {
+            X8(SAME8(BITOP3))
+        } else if constexpr (KIND == 4) {
+            X8(SAME8(ADD))
+        } else if constexpr (KIND == 5) {
+            X8(asm volatile("s_setprio 0\n\ts_setprio 0\n\ts_setprio 0\n\ts_setprio 0\n\t"
+                            "s_setprio 0\n\ts_setprio 0\n\ts_setprio 0\n\ts_setprio 0");)
+        } else if constexpr (KIND == 6) {
+            X8(CH8(PRIO_H, ALIGNBIT, ALIGNBIT, ALIGNBIT, PRIO_F, ADD, ADD, ADD))
+        } else {
+            X8(CH8(PRIO_H, ALIGNBIT, ALIGNBIT, ALIGNBIT, PRIO_FB, BITOP3, BITOP3, BITOP3))
+        }
+        ++it;
+        r = __builtin_amdgcn_s_memrealtime();
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if constexpr (KIND == 5 || KIND >= 6) __builtin_amdgcn_s_setprio(0);
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(kXccIdReg);
+    const uint32_t acc = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if ((threadIdx.x & 63) < 4) {
+        // the chains' value rides in the xcc word's upper half, so the compiler keeps every chain
+        const uint64_t v[4] = {it, t1 - t0, r - r0, (uint64_t)xcc | ((uint64_t)(acc & 0xffffu) << 32)};
+        out[4 * wave + (threadIdx.x & 63)] = v[threadIdx.x & 63];
+    }
+}
+
+using KernelFn = void (*)(uint64_t*, uint32_t, uint64_t);
+constexpr KernelFn kFns[] = {valu_energy<0>, valu_energy<1>, valu_energy<2>, valu_energy<3>,
+                             valu_energy<4>, valu_energy<5>, valu_energy<6>, valu_energy<7>};
+static_assert(sizeof(kFns) / sizeof(kFns[0]) == kNumKinds, "one kernel per kind");
+
+}  // namespace
+
+extern "C" int ve_kinds() { return kNumKinds; }
+extern "C" const char* ve_name(int k) { return k >= 0 && k < kNumKinds ? kKinds[k].name : nullptr; }
+extern "C" int ve_valu_per_iter(int k) { return k >= 0 && k < kNumKinds ? kKinds[k].valu : -1; }
+extern "C" int ve_salu_per_iter(int k) { return k >= 0 && k < kNumKinds ? kKinds[k].salu : -1; }
+
+extern "C" int ve_run(int dev, int kind, double seconds, int nwg, uint64_t* out) {
+    if (kind < 0 || kind >= kNumKinds || nwg < 1 || nwg > 65536 || !(seconds > 0 && seconds <= 30)) return -1;
+    if (hipSetDevice(dev) != hipSuccess) return -2;
+    uint64_t* d = nullptr;
+    const size_t bytes = sizeof(uint64_t) * 4 * 4 * (size_t)nwg;  // 4 waves per workgroup
+    if (hipMalloc(&d, bytes) != hipSuccess) return -3;
+    int rc = 0;
+    if (hipMemset(d, 0, bytes) != hipSuccess) rc = -4;
+    if (!rc) {
+        hipLaunchKernelGGL(kFns[kind], dim3(nwg), dim3(256), 0, 0, d, 0x2545f491u,
+                           (uint64_t)(seconds * 1e8));
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -5;
+    }
+    if (!rc && hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -6;
+    (void)hipFree(d);
+    return rc;
+}
