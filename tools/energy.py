@@ -204,8 +204,34 @@ class Window:
         return False
 
 
-def meter_for_device(dev):
-    """A Meter for HIP device `dev` (torch's device properties give its PCI address)."""
+def _loaded_hip():
+    """The HIP runtime this process already uses (its path from /proc/self/maps), or None: asking
+    a second copy of the runtime would initialise another HIP instance in the process."""
+    import ctypes
+    try:
+        for line in open("/proc/self/maps"):
+            path = line.split()[-1] if len(line.split()) >= 6 else ""
+            if "libamdhip64.so" in path:
+                return ctypes.CDLL(path)
+    except OSError:
+        pass
+    return None
+
+
+def pci_of_device(dev):
+    """(domain, bus, device) of HIP device `dev`: hipDeviceGetPCIBusId from the runtime already
+    loaded (libminehip's or torch's), else torch's device properties."""
+    import ctypes
+    hip = _loaded_hip()
+    if hip is not None:
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, ctypes.c_int(dev)) == 0:
+            return parse_bdf(buf.value.decode())
     import torch
     p = torch.cuda.get_device_properties(dev)
-    return Meter((p.pci_domain_id, p.pci_bus_id, p.pci_device_id))
+    return p.pci_domain_id, p.pci_bus_id, p.pci_device_id
+
+
+def meter_for_device(dev):
+    """A Meter for HIP device `dev`, found by its PCI address."""
+    return Meter(pci_of_device(dev))

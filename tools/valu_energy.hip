@@ -61,6 +61,8 @@ constexpr Kind kKinds[] = {
     {"setprio", 0, 64},        // scalar: the issue-priority markers alone
     {"h4f4_prio", 64, 16},     // 4 alignbit + 4 add with the product's markers (pairs issue)
     {"h4b4_prio", 64, 16},     // 4 alignbit + 4 bitop3 with markers
+    {"h4f4", 64, 0},           // the h4f4_prio stream without the markers
+    {"seg", 64, 0},            // class-segregated waves: even waves alignbit only, odd waves add only
 };
 constexpr int kNumKinds = sizeof(kKinds) / sizeof(kKinds[0]);
 
@@ -87,14 +89,22 @@ __global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, u
                             "s_setprio 0\n\ts_setprio 0\n\ts_setprio 0\n\ts_setprio 0");)
         } else if constexpr (KIND == 6) {
             X8(CH8(PRIO_H, ALIGNBIT, ALIGNBIT, ALIGNBIT, PRIO_F, ADD, ADD, ADD))
-        } else {
+        } else if constexpr (KIND == 7) {
             X8(CH8(PRIO_H, ALIGNBIT, ALIGNBIT, ALIGNBIT, PRIO_FB, BITOP3, BITOP3, BITOP3))
+        } else if constexpr (KIND == 8) {
+            X8(CH8(ALIGNBIT, ALIGNBIT, ALIGNBIT, ALIGNBIT, ADD, ADD, ADD, ADD))
+        } else {
+            if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) & 1u) {
+                X8(SAME8(ADD))
+            } else {
+                X8(SAME8(ALIGNBIT))
+            }
         }
         ++it;
         r = __builtin_amdgcn_s_memrealtime();
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
-    if constexpr (KIND == 5 || KIND >= 6) __builtin_amdgcn_s_setprio(0);
+    if constexpr (KIND == 5 || KIND == 6 || KIND == 7) __builtin_amdgcn_s_setprio(0);
     const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(kXccIdReg);
     const uint32_t acc = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
@@ -106,8 +116,8 @@ __global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, u
 }
 
 using KernelFn = void (*)(uint64_t*, uint32_t, uint64_t);
-constexpr KernelFn kFns[] = {valu_energy<0>, valu_energy<1>, valu_energy<2>, valu_energy<3>,
-                             valu_energy<4>, valu_energy<5>, valu_energy<6>, valu_energy<7>};
+constexpr KernelFn kFns[] = {valu_energy<0>, valu_energy<1>, valu_energy<2>, valu_energy<3>, valu_energy<4>,
+                             valu_energy<5>, valu_energy<6>, valu_energy<7>, valu_energy<8>, valu_energy<9>};
 static_assert(sizeof(kFns) / sizeof(kFns[0]) == kNumKinds, "one kernel per kind");
 
 }  // namespace
