@@ -337,8 +337,16 @@ def _check_n2_line(line, driver):
     assert line["roofline"]["frac"] and 0 < line["roofline"]["frac"] <= 1
     for p in line["per_device"]:
         assert p["dev"] == 0 and p["nonces"] > 0 and p["kernel_clock_ghz"] and 1.0 < p["kernel_clock_ghz"] <= 2.5, p
+        # each device's socket power and J per 10^9 nonces of the same
+        # concurrent search, and the limit that held its clock
+        e = p["energy"]
+        assert e and 100 < e["mean_w"] < 2000 and 5 < e["j_per_gnonce"] < 200, e
+        assert e["kernel_clock_ghz"] == p["kernel_clock_ghz"] and e["limiter"], e
     lo, hi = line["kernel_clock_ghz_range"]
     assert 1.0 < lo <= hi <= 2.5
+    wlo, whi = line["power_w_range"]
+    jlo, jhi = line["j_per_gnonce_range"]
+    assert 100 < wlo <= whi < 2000 and 5 < jlo <= jhi < 200
 
 
 @pytest.mark.gpu

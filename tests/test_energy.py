@@ -1,0 +1,117 @@
+"""The energy plumbing of the bench line and the fixed-power model, on CPU with stubs (VERDICT r05
+items 1-2): tools/energy.py's window arithmetic and limiter choice, bench.energy_fields, the
+per-device energy of the N > 1 paths (bench.kernel_clocks with meters), and tools/energy_model.py's
+fit recovering known parameters."""
+import math
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tools")]
+import bench  # noqa: E402
+import energy  # noqa: E402
+import energy_model  # noqa: E402
+
+
+def _read(ns, joules, acc, ppt, thm=0):
+    return {"host_ns": ns, "energy_j": joules, "energy_ts": ns,
+            "viol": {"acc_counter": acc, "acc_ppt_pwr": ppt, "acc_socket_thrm": thm, "acc_vr_thrm": 0,
+                     "acc_hbm_thrm": 0, "acc_prochot_thrm": 0, "acc_gfx_clk_below_host_limit": 0}}
+
+
+def test_window_delta_energy_power_and_limiter():
+    a, b = _read(0, 1000.0, 100, 10), _read(2_000_000_000, 3640.0, 300, 110)
+    d = energy.window_delta(a, b, nonces=1 << 37)
+    assert d["seconds"] == 2.0 and d["joules"] == 2640.0 and d["mean_w"] == 1320.0
+    assert d["j_per_gnonce"] == round(2640.0 / ((1 << 37) / 1e9), 4)
+    assert d["limit_active_share"]["ppt_pwr"] == 0.5 and d["limiter"] == "ppt_pwr"
+    quiet = energy.window_delta(_read(0, 0.0, 0, 0), _read(10 ** 9, 400.0, 100, 1))
+    assert quiet["limiter"] == "none reported" and "j_per_gnonce" not in quiet
+    hot = energy.window_delta(_read(0, 0.0, 0, 0, 0), _read(10 ** 9, 400.0, 100, 0, 30))
+    assert hot["limiter"] == "socket_thrm"
+    bare = energy.window_delta({"host_ns": 0, "energy_error": "x"}, {"host_ns": 1})
+    assert bare["energy_error"] == "x" and bare["limiter"] == "not exposed"
+
+
+def test_parse_bdf():
+    assert energy.parse_bdf("0000:75:00.0") == (0, 0x75, 0)
+    assert energy.parse_bdf("0001:e5:1f.1\n") == (1, 0xE5, 0x1F)
+
+
+class StubMeter:
+    """A meter whose counters advance by `watts` per second of host time."""
+    ok = True
+    error = None
+
+    def __init__(self, watts):
+        self.watts = watts
+
+    def read(self):
+        import time
+        t = time.perf_counter_ns()
+        return _read(t, self.watts * t * 1e-9, t // 1000, t // 2000)
+
+    def snapshot(self):
+        return {"current_socket_power": self.watts, "power_limit_w": 1400.0, "gfx_clk_mhz": [2200] * 8}
+
+
+def test_window_and_energy_fields():
+    w = energy.Window(StubMeter(1300.0), nonces=10 ** 9, snap_after_s=0.01)
+    import time
+    with w:
+        time.sleep(0.05)
+    r = w.result
+    assert abs(r["mean_w"] - 1300.0) < 1.0 and r["limiter"] == "ppt_pwr" and r["snapshot"]["power_limit_w"] == 1400.0
+    f = bench.energy_fields(r, {"ghz": 2.2})
+    assert f["kernel_clock_ghz"] == 2.2 and abs(f["j_per_gnonce"] - r["joules"]) < 1e-3
+    assert f["power_limit_w"] == 1400.0 and f["limiter"] == "ppt_pwr"
+    assert bench.energy_fields(None)["error"] and bench.energy_fields({"energy_error": "e"})["error"] == "e"
+    # no meter at all: the Window still ends and says why
+    w2 = energy.Window(None)
+    with w2:
+        pass
+    assert w2.result["error"]
+
+
+def test_kernel_clocks_pass_each_device_its_meter():
+    """The in-process N > 1 line: one thread per device, each probe gets its own device's meter
+    and returns its energy beside its clock (bench.py copies both into per_device)."""
+    seen = {}
+
+    def probe(search_dev, dev, meter=None):
+        seen[dev] = meter
+        return {"ghz": 2.0 + dev / 100, "energy": {"mean_w": meter.watts, "j_per_gnonce": 24.0 + dev}}
+
+    meters = {d: StubMeter(1300.0 + d) for d in (0, 1, 3)}
+    out = bench.kernel_clocks(lambda d: (lambda m, a, b: None), [0, 1, 1, 3], probe=probe, meters=meters)
+    assert {d: seen[d].watts for d in seen} == {0: 1300.0, 1: 1301.0, 3: 1303.0}
+    assert out[3]["energy"]["j_per_gnonce"] == 27.0 and out[1]["ghz"] == 2.01
+
+
+def test_model_fit_recovers_known_parameters():
+    """Points generated from P - floor = c f^kappa (H + rho F + sigma S) / Q are fitted back."""
+    kappa, rho, sigma, lnc, floor = 2.6, 0.8, 0.03, math.log(0.05), 370.0
+    pts = []
+    for s, q in ((0, 720.0), (33, 700.0), (50, 690.0), (67, 675.0), (100, 680.0)):
+        H, F, S = 703 - s, 493 + 2 * s, 400 + s // 3
+        A = (H + rho * F + sigma * S) / q
+        p_cap = 1320.0 + s * 0.05
+        f = math.exp((math.log(p_cap - floor) - lnc - math.log(A)) / kappa)
+        pts.append({"H": H, "F": F, "S": S, "Q": q, "f": f, "P": p_cap})
+    rms, c, k, r = energy_model.fit(pts, sigma, floor)
+    assert rms < 1e-3 and abs(k - kappa) < 0.05 and abs(r - rho) < 0.02
+    m = {"ln_c": c, "kappa": k, "rho": r, "sigma": sigma, "floor_w": floor}
+    f, R = energy_model.predict(m, pts[3]["H"], pts[3]["F"], pts[3]["S"], pts[3]["Q"], pts[3]["P"])
+    assert abs(f / pts[3]["f"] - 1) < 2e-3 and abs(R - f * 16384 / pts[3]["Q"]) < 1e-9
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "build", "fast_search_prio.s")),
+                    reason="needs the built assembly (make all)")
+def test_loop_counts_of_the_product():
+    """The product loop's classes as the model counts them: fast_search<4, One> per 64 nonces."""
+    c = energy_model.loop_counts(os.path.join(ROOT, "build", "fast_search_prio.s"))
+    assert c["H"] + c["F"] == 1263 and c["H"] == 636 and c["S"] > 0
+    assert c["ops"]["v_alignbit_b32"] == 500 and c["ops"]["v_add3_u32"] == 134

@@ -139,10 +139,10 @@ class Meter:
 
 def window_delta(a, b, nonces=None):
     """Energy, mean power and the share of the window each limit was active, between two reads."""
-    out = {"seconds": round((b["host_ns"] - a["host_ns"]) * 1e-9, 4)}
+    sec = (b["host_ns"] - a["host_ns"]) * 1e-9
+    out = {"seconds": round(sec, 4)}
     if "energy_j" in a and "energy_j" in b:
         j = b["energy_j"] - a["energy_j"]
-        sec = out["seconds"]
         if a.get("energy_ts") and b.get("energy_ts") and b["energy_ts"] > a["energy_ts"]:
             # the firmware's own timestamps of the two readings (ns), when it gives them
             fw = (b["energy_ts"] - a["energy_ts"]) * 1e-9

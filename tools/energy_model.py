@@ -1,0 +1,210 @@
+"""tools/energy_model.py -- the add3 split (and the other loop variants) priced under a fixed power
+budget instead of the issue bound max(H, N/2).
+
+The fast kernel runs at the firmware's package-power limit (PPT active for about half of every
+window, `roofline.energy.limit_active_share`), so a variant's clock is set by how much power its
+instruction stream draws per cycle, and its rate is clock / quad-cycles per nonce.  The model:
+
+    P - P_floor = c * f^kappa * A,     A = (H + rho * F + sigma * S) / Q
+
+  P        socket power at the limit (each variant's own mean W over its energy window)
+  P_floor  the chip with every wave slot resident but idle (tools/valu_energy.hip "sleep")
+  f        the kernel clock read inside the GPU during the same window (tools/clock_probe.hip)
+  H, F, S  half-rate VALU, full-rate VALU and s_setprio instructions per 64 nonces (one wave
+           iteration of the per-nonce loop, counted in the variant's assembly)
+  Q        SIMD quad-cycles per 64 nonces, measured (kbench: clock / search rate)
+  kappa    how power per unit of activity grows with the clock (f * V(f)^2: 1 + 2 * gamma when the
+           voltage goes as f^gamma); rho, sigma the energy of a full-rate VALU instruction and of a
+           marker against a half-rate one, inside the kernel's own mixed stream
+
+kappa and rho are fitted on the variants of one A/B (same box, same process); sigma is taken from
+the probes (a marker against an alignbit, each in a stream of its own).  The fixed-power rate of a
+variant is then R = f / Q with f = ((P_cap - P_floor) / (c A))^(1/kappa): at a fixed budget a
+variant wins by issuing its nonces in fewer quad-cycles only as far as the energy per quad-cycle
+it adds does not cost more clock.  The same fit predicts round 3's split result (HISTORY.md §4:
+none -> every third add3 split: quad-cycles 720 -> 675 per 64 nonces, clock -4.6%, rate +1.9% on
+the d = 10 bucket) from round 3's quad-cycles alone, and ranks split counts the A/B did not build.
+
+  python tools/energy_model.py --ab profiles/r06b_kbench_energy_split.json \\
+      --probe profiles/r06a_energy_probe.json [--out profiles/r06b_energy_model.json]
+
+Counting the loops needs the variants' assembly: `python tools/isa_variant.py prio a3split6 ...`
+(build/isa/<variant>.s); the product build is build/fast_search_prio.s.
+"""
+import argparse
+import collections
+import json
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bitcoin-miner_amd", "csrc"))
+
+KERNEL = "_ZN2mh11fast_searchILi4ELi0EE"  # fast_search<4, One>: configs[1]'s d = 10 bucket
+SIMDS = 1024
+
+
+def loop_counts(s_path, kernel=KERNEL):
+    """(H, F, S) of the kernel's per-nonce loop in an assembly file, plus the opcode histogram."""
+    import loop_mix
+    from valu_rates import valu_rate
+    for name, body in loop_mix.kernels(open(s_path).read()).items():
+        if name.startswith(kernel):
+            ins = loop_mix.inner_loop(body)
+            valu = [x for x in ins if x != "s_setprio"]
+            h = sum(1 for x in valu if valu_rate(x) == "H")
+            return {"H": h, "F": len(valu) - h, "S": ins.count("s_setprio"),
+                    "ops": dict(collections.Counter(ins).most_common())}
+    raise SystemExit(f"{kernel} not in {s_path}")
+
+
+def variant_asm(name):
+    if name == "product":
+        return os.path.join(ROOT, "build", "fast_search_prio.s")
+    return os.path.join(ROOT, "build", "isa", f"{name}.s")
+
+
+def probe_prices(probe):
+    """pJ per wave-instruction of each probe class over the sleep floor, from an energy_probe.json
+    (the median over its rounds), and the floor / idle watts."""
+    rows = collections.defaultdict(list)
+    for rnd in probe["rounds"]:
+        for r in rnd:
+            rows[r.get("kind")].append(r)
+
+    def med(v):
+        v = sorted(v)
+        return v[len(v) // 2]
+
+    floor = med([r["mean_w"] for r in rows["sleep"]])
+    out = {"floor_w": floor, "idle_w": med([r["mean_w"] for r in rows["idle"]]) if rows["idle"] else None,
+           "floor_clock_ghz": med([r["clock_ghz"] for r in rows["sleep"]]), "pj_per_wave_instr": {},
+           "classes": {}}
+    for k, rs in rows.items():
+        if k in ("idle", "sleep") or not k or k.startswith("product"):
+            continue
+        w = med([r["mean_w"] for r in rs])
+        n = med([(r.get("valu_wave_instr_per_s") or 0) + (r.get("salu_wave_instr_per_s") or 0) for r in rs])
+        out["classes"][k] = {"mean_w": w, "clock_ghz": med([r["clock_ghz"] for r in rs]),
+                             "valu_per_simd_quad": med([r.get("valu_per_simd_quad") or 0 for r in rs]),
+                             "ppt_share": med([(r.get("limit_active_share") or {}).get("ppt_pwr", 0) for r in rs])}
+        if n:
+            out["pj_per_wave_instr"][k] = round((w - floor) / n * 1e12, 1)
+    return out
+
+
+def fit(points, sigma, floor):
+    """Least squares of ln(P - floor) = ln c + kappa ln f + ln A(rho) over a grid of rho.
+    points: [{"H", "F", "S", "Q", "f", "P"}].  Returns (rms, ln c, kappa, rho)."""
+    best = None
+    for i in range(1, 601):
+        rho = i / 200  # 0.005 .. 3.0
+        xs = [math.log(p["f"]) for p in points]
+        ys = [math.log(p["P"] - floor) - math.log((p["H"] + rho * p["F"] + sigma * p["S"]) / p["Q"]) for p in points]
+        n = len(xs)
+        mx, my = sum(xs) / n, sum(ys) / n
+        sxx = sum((x - mx) ** 2 for x in xs)
+        if sxx <= 0:
+            continue
+        kappa = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx
+        lnc = my - kappa * mx
+        rms = math.sqrt(sum((y - lnc - kappa * x) ** 2 for x, y in zip(xs, ys)) / n)
+        if kappa > 0 and (best is None or rms < best[0]):
+            best = (rms, lnc, kappa, rho)
+    return best
+
+
+def predict(m, H, F, S, Q, p_cap):
+    """Clock (GHz) and rate (GH/s) of a loop at the budget p_cap under model m."""
+    A = (H + m["rho"] * F + m["sigma"] * S) / Q
+    f = math.exp((math.log(p_cap - m["floor_w"]) - m["ln_c"] - math.log(A)) / m["kappa"])
+    return f, f * 1e9 * SIMDS * 16 / Q / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ab", required=True, help="kbench JSON with --energy rounds per variant")
+    ap.add_argument("--probe", required=True, help="energy_probe.json")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    ab = json.load(open(a.ab))
+    pr = probe_prices(json.load(open(a.probe)))
+    pj = pr["pj_per_wave_instr"]
+    sigma = pj.get("setprio", 0.0) / pj["alignbit"] if pj.get("alignbit") else 0.0
+    points, skipped = {}, {}
+    for name, v in ab.items():
+        e = v.get("energy") or {}
+        if not (e.get("ghz_med") and e.get("mean_w_med") and e.get("simd_quads_per_64_nonces")):
+            skipped[name] = "no energy rounds"
+            continue
+        path = variant_asm(name)
+        if not os.path.exists(path):
+            skipped[name] = f"no assembly {os.path.relpath(path, ROOT)}"
+            continue
+        c = loop_counts(path)
+        points[name] = dict(c, Q=e["simd_quads_per_64_nonces"], f=e["ghz_med"], P=e["mean_w_med"],
+                            R=e["search_ghs_med"], j_per_gnonce=e.get("j_per_gnonce_med"),
+                            wall_ghs_med=v.get("wall_ghs_med"), limiters=e.get("limiters"))
+    # occupancy variants share the product's mix but not its register budget: fitted like the rest
+    rms, lnc, kappa, rho = fit(list(points.values()), sigma, pr["floor_w"])
+    m = {"ln_c": lnc, "kappa": kappa, "rho": rho, "sigma": sigma, "floor_w": pr["floor_w"], "rms_ln": rms}
+    p_cap = sorted(p["P"] for p in points.values())[len(points) // 2]
+    for p in points.values():
+        f, R = predict(m, p["H"], p["F"], p["S"], p["Q"], p["P"])
+        p["model_ghz"], p["model_ghs"] = round(f, 4), round(R, 3)
+
+    # round 3's split A/B (HISTORY.md §4, profiles/r03n_*, r03o_*): quad-cycles per 64 nonces 720 / 675
+    # at 2.301 / 2.196 GHz, the d = 10 bucket +1.9%; its loops had this build's mixes
+    ns, sp = points.get("nosplit"), points.get("a3split3") or points.get("product")
+    r3 = None
+    if ns and sp:
+        f0, R0 = predict(m, ns["H"], ns["F"], ns["S"], 720.0, p_cap)
+        f1, R1 = predict(m, sp["H"], sp["F"], sp["S"], 675.0, p_cap)
+        r3 = {"clock_change_pred": round(f1 / f0 - 1, 4), "clock_change_meas": round(2.196 / 2.301 - 1, 4),
+              "rate_change_pred": round(R1 / R0 - 1, 4), "rate_change_meas_d10": 0.019,
+              "rate_change_meas_range": [0.020, 0.026],
+              "within_1pct": abs((R1 / R0 - 1) - 0.019) <= 0.01}
+
+    # every split count s of the 201 add3 (continuous), Q from the issue bound with the pairing
+    # efficiency interpolated between the built variants
+    ranking = None
+    if ns:
+        built = sorted(((ns["H"] - p["H"], p) for n, p in points.items() if n != "split_w8" and p["F"] - ns["F"]
+                        == 2 * (ns["H"] - p["H"])), key=lambda t: t[0])
+        eff = [(s, max(p["H"], (p["H"] + p["F"]) / 2) / p["Q"]) for s, p in built]
+
+        def eta(s):
+            for (s0, e0), (s1, e1) in zip(eff, eff[1:]):
+                if s0 <= s <= s1:
+                    return e0 + (e1 - e0) * (s - s0) / (s1 - s0) if s1 > s0 else e0
+            return eff[0][1] if s < eff[0][0] else eff[-1][1]
+
+        def s_markers(s):
+            for (s0, p0), (s1, p1) in zip(built, built[1:]):
+                if s0 <= s <= s1:
+                    return p0["S"] + (p1["S"] - p0["S"]) * (s - s0) / (s1 - s0) if s1 > s0 else p0["S"]
+            return built[0][1]["S"] if s < built[0][0] else built[-1][1]["S"]
+
+        rows = []
+        for s in range(0, 202):  # the nosplit loop's 201 add3 (its H also holds the alignbits)
+            H, F = ns["H"] - s, ns["F"] + 2 * s
+            Q = max(H, (H + F) / 2) / eta(s)
+            f, R = predict(m, H, F, s_markers(s), Q, p_cap)
+            rows.append({"split": s, "H": H, "N": H + F, "Q": round(Q, 1), "ghz": round(f, 4), "ghs": round(R, 3)})
+        top = max(rows, key=lambda r: r["ghs"])
+        ranking = {"best": top, "every_third": next(r for r in rows if r["split"] == 67),
+                   "issue_bound_best": min(rows, key=lambda r: max(r["H"], r["N"] / 2))["split"],
+                   "curve": rows[::6]}
+    out = {"model": m, "p_cap_w": p_cap, "probe": pr, "points": points, "skipped": skipped,
+           "round3_split": r3, "split_ranking": ranking,
+           "note": "P - P_floor = c f^kappa (H + rho F + sigma S) / Q, fitted on one A/B's variants "
+                   "(tools/energy_model.py)"}
+    s = json.dumps(out, indent=1)
+    if a.out:
+        open(a.out, "w").write(s)
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
