@@ -40,7 +40,7 @@ $(LIB): $(SRCS) $(HDRS) $(FAST_O)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -x none $(FAST_O)
 
 # dev build: the same library plus the experiment / test hooks (MINEHIP_DEV_CODE_OBJECT,
-# MINEHIP_DEV_LDS, MINEHIP_TEST_FAIL_WORKER).  Never the package's library: tools and the
+# MINEHIP_DEV_LDS, MINEHIP_TEST_FAIL_WORKER, MINEHIP_TEST_SPAWN_LIMIT).  Never the package's library: tools and the
 # tests that need a hook load it explicitly (MINEHIP_LIB=build/dev/libminehip.so).
 dev: $(DEVLIB)
 $(DEVLIB): $(SRCS) $(HDRS) $(FAST_O)

@@ -33,7 +33,7 @@ def test_exports_every_declared_symbol():
 def test_product_library_has_no_dev_hooks():
     """The experiment and test hooks (code-object override, LDS cap, injected worker failure)
     exist only in the dev build (`make dev`), never in the package's library (VERDICT r02 #6)."""
-    hooks = (b"MINEHIP_DEV_CODE_OBJECT", b"MINEHIP_DEV_LDS", b"MINEHIP_TEST_FAIL_WORKER")
+    hooks = (b"MINEHIP_DEV_CODE_OBJECT", b"MINEHIP_DEV_LDS", b"MINEHIP_TEST_FAIL_WORKER", b"MINEHIP_TEST_SPAWN_LIMIT")
     prod = open(_lib.PRODUCT_LIB_PATH, "rb").read()
     assert not [h for h in hooks if h in prod]
     from conftest import DEV_LIB

@@ -105,3 +105,28 @@ for chunk in (1 << 27, 0):
     assert r.returncode == 0, r.stderr[-2000:]
     lines = r.stdout.strip().splitlines()[-2:]
     assert [tuple(int(x) for x in ln.split()) for ln in lines] == [exp, exp]
+
+
+def test_search_multi_thread_start_failure(gpu):
+    """Host threads that cannot start: with the dev build's MINEHIP_TEST_SPAWN_LIMIT=k
+    only the first k workers' threads start.  k > 0: the started workers take the others' shards
+    (adaptive) or chunks (fixed) and the answer is unchanged; k = 0: MH_EINTERNAL, nothing searched."""
+    from conftest import run_dev
+    hi = (1 << 31) - 1
+    exp = gpu.search("cmu440", 0, hi)
+    r = run_dev(f"""
+import os, minehip
+os.environ["MINEHIP_TEST_SPAWN_LIMIT"] = "1"
+print(*minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0, 0], chunk=1 << 27))
+print(*minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0, 0]))
+os.environ["MINEHIP_TEST_SPAWN_LIMIT"] = "0"
+for chunk in (1 << 27, 0):
+    try:
+        minehip.search_multi("cmu440", 0, {hi}, devs=[0, 0], chunk=chunk)
+        raise SystemExit("search_multi succeeded with no worker thread started")
+    except minehip.MinehipError as e:
+        assert e.code == minehip.MH_EINTERNAL and "could not start" in str(e), e
+""")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()[-2:]
+    assert [tuple(int(x) for x in ln.split()) for ln in lines] == [exp, exp]
