@@ -59,9 +59,13 @@ def loop_counts(s_path, kernel=KERNEL):
     raise SystemExit(f"{kernel} not in {s_path}")
 
 
-def variant_asm(name):
+def variant_asm(name, recipe=None):
+    """The assembly of an A/B variant: the product build, or the code object the recipe names."""
     if name == "product":
         return os.path.join(ROOT, "build", "fast_search_prio.s")
+    co = (recipe or {}).get("code_objects", {}).get(name)
+    if co:
+        return os.path.join(ROOT, co[:-len(".hsaco")] + ".s")
     return os.path.join(ROOT, "build", "isa", f"{name}.s")
 
 
@@ -126,9 +130,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ab", required=True, help="kbench JSON with --energy rounds per variant")
     ap.add_argument("--probe", required=True, help="energy_probe.json")
+    ap.add_argument("--recipe", default=os.path.join(ROOT, "tools", "ab", "r06_energy_split.json"),
+                    help="the A/B recipe (maps variant names to code objects)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ab = json.load(open(a.ab))
+    recipe = json.load(open(a.recipe)) if a.recipe and os.path.exists(a.recipe) else None
     pr = probe_prices(json.load(open(a.probe)))
     pj = pr["pj_per_wave_instr"]
     sigma = pj.get("setprio", 0.0) / pj["alignbit"] if pj.get("alignbit") else 0.0
@@ -138,7 +145,7 @@ def main():
         if not (e.get("ghz_med") and e.get("mean_w_med") and e.get("simd_quads_per_64_nonces")):
             skipped[name] = "no energy rounds"
             continue
-        path = variant_asm(name)
+        path = variant_asm(name, recipe)
         if not os.path.exists(path):
             skipped[name] = f"no assembly {os.path.relpath(path, ROOT)}"
             continue

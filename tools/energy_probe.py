@@ -7,9 +7,10 @@ One process on one GPU (run on the box, after `make all`):
 
   1. what amdsmi exposes (energy counter, limit accumulators, metrics; `amd-smi metric --help`);
   2. an idle window (no kernel);
-  3. every probe of tools/valu_energy.hip (build/libvaluenergy.so): 8 waves per SIMD on every CU
-     running one instruction class for a fixed wall time, bracketed by the socket's energy counter
-     and the limit accumulators, with a mid-window snapshot of voltage, power and per-XCD clocks;
+  3. every probe of tools/valu_energy.hip (build/libvaluenergy.so): 8 waves per SIMD on every CU,
+     all started together, running one instruction class for a fixed wall time, with the socket's
+     energy counter and the limit accumulators read inside that time and a snapshot of power and
+     per-XCD clocks in its middle;
   4. the product: a 2^37-nonce search of fast_search<4, One> with the in-kernel clock probe
      (bench.kernel_clock with an energy window), the figure bench.py reports as roofline.energy.
 
@@ -35,15 +36,30 @@ def median(v):
     return v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2 - 1] + v[len(v) // 2]) / 2
 
 
-def run_probe(lib, meter, kind, seconds, nwg, dev=0):
+def run_probe(lib, meter, kind, seconds, nwg, dev=0, delay=1.0, margin=0.1):
+    """One probe: every wave sleeps until `delay` after the launch, then runs its stream for
+    `seconds`; the energy window is [start + margin, end - margin], inside the stream, with one
+    metrics snapshot in its middle.  Rates come from every wave's own count over the stream."""
     import energy
     nw = 4 * nwg
     buf = (ctypes.c_uint64 * (4 * nw))()
-    w = energy.Window(meter, snap_after_s=seconds / 2)
-    with w:
-        rc = lib.ve_run(dev, kind, seconds, nwg, buf)
+    rc = lib.ve_start(dev, kind, delay, seconds, nwg)
     if rc != 0:
-        return {"error": f"ve_run rc {rc}"}
+        return {"error": f"ve_start rc {rc}"}
+    t0 = time.perf_counter()
+    try:
+        time.sleep(max(0.0, t0 + delay + margin - time.perf_counter()))
+        a = meter.read()
+        time.sleep(max(0.0, t0 + delay + seconds / 2 - time.perf_counter()))
+        snap = meter.snapshot()
+        time.sleep(max(0.0, t0 + delay + seconds - margin - time.perf_counter()))
+        b = meter.read()
+    finally:
+        rc = lib.ve_wait(dev, buf, nwg)  # always: waits for the kernel and frees its buffer
+    if rc != 0:
+        return {"error": f"ve_wait rc {rc}"}
+    res = energy.window_delta(a, b)
+    res["snapshot"] = snap
     rows = [tuple(buf[4 * i:4 * i + 4]) for i in range(nw)]
     iters = sum(r[0] for r in rows)
     ghz = [r[1] / (r[2] / 1e8) / 1e9 for r in rows if r[2]]
@@ -51,17 +67,19 @@ def run_probe(lib, meter, kind, seconds, nwg, dev=0):
     for r in rows:
         if r[2]:
             by_xcd.setdefault(int(r[3] & 0xffffffff), []).append(r[1] / (r[2] / 1e8) / 1e9)
-    loop_s = median([r[2] / 1e8 for r in rows if r[2]])
+    ticks = sorted(r[2] for r in rows)
+    stream_s = median(ticks) / 1e8
     valu, salu = lib.ve_valu_per_iter(kind), lib.ve_salu_per_iter(kind)
-    res = dict(w.result)
     res.update({
-        "kind": lib.ve_name(kind).decode(), "waves": nw, "loop_s": round(loop_s, 4),
+        "kind": lib.ve_name(kind).decode(), "waves": nw, "stream_s": round(stream_s, 4),
+        # every wave ran the same [start, end]: the shortest and longest stream show it
+        "stream_s_range": [round(ticks[0] / 1e8, 4), round(ticks[-1] / 1e8, 4)],
         "clock_ghz": round(median(ghz), 4) if ghz else None,
         "clock_ghz_by_xcd": {str(x): round(median(v), 4) for x, v in sorted(by_xcd.items())},
         "wave_iterations": iters,
         "valu_wave_instr": iters * valu, "salu_wave_instr": iters * salu,
-        "valu_wave_instr_per_s": iters * valu / loop_s if loop_s else None,
-        "salu_wave_instr_per_s": iters * salu / loop_s if loop_s else None,
+        "valu_wave_instr_per_s": iters * valu / stream_s if stream_s else None,
+        "salu_wave_instr_per_s": iters * salu / stream_s if stream_s else None,
     })
     if res.get("valu_wave_instr_per_s") and res.get("clock_ghz"):
         # VALU instructions per SIMD quad-cycle (2 = the issue peak of a pair every quad)
@@ -117,7 +135,8 @@ def main():
 
     lib = ctypes.CDLL(os.path.join(ROOT, "build", "libvaluenergy.so"))
     lib.ve_name.restype = ctypes.c_char_p
-    lib.ve_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    lib.ve_start.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
+    lib.ve_wait.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     nwg = a.nwg or 8 * cus
     kinds = [k for k in range(lib.ve_kinds())

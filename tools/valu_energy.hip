@@ -3,11 +3,14 @@
 //
 // Each kernel keeps every SIMD of the chip at 8 waves, each wave running ONE instruction class
 // (inline asm pins the encoding) over 8 independent register chains, 64 instructions per
-// iteration, until a fixed wall time has passed (s_memrealtime, 100 MHz), so every probe lasts as
-// long as the energy window around it whatever clock the chip holds.  Every wave records its
-// iterations, its shader cycles and 100 MHz ticks over the loop, and its XCD; the host (tools/
-// energy_probe.py) brackets the launch with the socket's energy counter and turns the counts into
-// wave-instructions per second and the clock the chip held.
+// iteration, between two absolute times of the 100 MHz counter (s_memrealtime) that the host
+// derives from a timestamp kernel: every wave sleeps until the start time, so all of them are
+// resident and start together (a wave launched into a SIMD whose older waves already saturate the
+// VALU would otherwise wait for them: a time-per-wave loop then runs in generations), and runs its
+// stream until the end time.  Every wave records its iterations, its shader cycles and 100 MHz
+// ticks over the stream, and its XCD; the host (tools/energy_probe.py) reads the socket's energy
+// counter inside [start, end] while the kernel runs and turns the counts into wave-instructions per
+// second and the clock the chip held.
 //
 // The operands toggle like the SHA-256 loop's: rotations of a running value, sums and three-way
 // xors with per-lane values.  Results go to a buffer of their own by vector stores (lane 0 of
@@ -17,10 +20,11 @@
 //   ve_kinds()                                        number of probe kinds
 //   ve_name(kind)                                     its name
 //   ve_valu_per_iter(kind), ve_salu_per_iter(kind)    instructions per wave-iteration
-//   ve_run(dev, kind, seconds, nwg, out)              launch nwg workgroups of 256 threads on
-//                                                     device dev and wait; out[4*w..4*w+3] =
-//                                                     {iterations, cycles, 100 MHz ticks, xcc} of
-//                                                     wave w (nwg*4 waves)
+//   ve_start(dev, kind, delay_s, seconds, nwg)        launch nwg workgroups of 256 threads on
+//                                                     device dev, their stream from delay_s after
+//                                                     the call for seconds; returns at once
+//   ve_wait(dev, out, nwg)                            wait for it; out[4*w..4*w+3] = {iterations,
+//                                                     cycles, 100 MHz ticks, xcc} of wave w
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -66,14 +70,24 @@ constexpr Kind kKinds[] = {
 };
 constexpr int kNumKinds = sizeof(kKinds) / sizeof(kKinds[0]);
 
+__global__ void realtime_now(uint64_t* __restrict__ out) {
+    if (threadIdx.x == 0) out[0] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <int KIND>
-__global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, uint32_t s, uint64_t ticks) {
+__global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, uint32_t s, uint64_t r_start,
+                                                   uint64_t r_end) {
     uint32_t x0 = (threadIdx.x * 0x9e3779b9u) ^ s, x1 = x0 * 3u + 1u, x2 = x0 * 5u + 7u, x3 = x0 * 7u + 11u,
              x4 = x0 * 9u + 13u, x5 = x0 * 11u + 17u, x6 = x0 * 13u + 19u, x7 = x0 * 15u + 23u;
     const uint32_t y = (threadIdx.x + s) * 0x85ebca6bu, z = (threadIdx.x ^ 0x5bd1e995u) * 0xc2b2ae35u;
-    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t r = r0, it = 0;
-    while (r - r0 < ticks) {
+    uint64_t r = __builtin_amdgcn_s_memrealtime();
+    while (r < r_start) {  // every wave resident and asleep until the common start
+        __builtin_amdgcn_s_sleep(127);
+        r = __builtin_amdgcn_s_memrealtime();
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = r;
+    uint64_t it = 0;
+    while (r < r_end) {
         if constexpr (KIND == 0) {
             __builtin_amdgcn_s_sleep(8);
         } else if constexpr (KIND == 1) {
@@ -115,7 +129,7 @@ __global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, u
     }
 }
 
-using KernelFn = void (*)(uint64_t*, uint32_t, uint64_t);
+using KernelFn = void (*)(uint64_t*, uint32_t, uint64_t, uint64_t);
 constexpr KernelFn kFns[] = {valu_energy<0>, valu_energy<1>, valu_energy<2>, valu_energy<3>, valu_energy<4>,
                              valu_energy<5>, valu_energy<6>, valu_energy<7>, valu_energy<8>, valu_energy<9>};
 static_assert(sizeof(kFns) / sizeof(kFns[0]) == kNumKinds, "one kernel per kind");
@@ -127,20 +141,50 @@ extern "C" const char* ve_name(int k) { return k >= 0 && k < kNumKinds ? kKinds[
 extern "C" int ve_valu_per_iter(int k) { return k >= 0 && k < kNumKinds ? kKinds[k].valu : -1; }
 extern "C" int ve_salu_per_iter(int k) { return k >= 0 && k < kNumKinds ? kKinds[k].salu : -1; }
 
-extern "C" int ve_run(int dev, int kind, double seconds, int nwg, uint64_t* out) {
-    if (kind < 0 || kind >= kNumKinds || nwg < 1 || nwg > 65536 || !(seconds > 0 && seconds <= 30)) return -1;
+constexpr int kMaxDevices = 64;
+struct Slot {
+    uint64_t* out = nullptr;  // non-null while a probe is outstanding
+    int nwg = 0;
+};
+Slot g_slot[kMaxDevices];
+
+extern "C" int ve_start(int dev, int kind, double delay_s, double seconds, int nwg) {
+    if (dev < 0 || dev >= kMaxDevices || g_slot[dev].out) return -1;
+    if (kind < 0 || kind >= kNumKinds || nwg < 1 || nwg > 65536 || !(seconds > 0 && seconds <= 30) ||
+        !(delay_s >= 0 && delay_s <= 10))
+        return -1;
     if (hipSetDevice(dev) != hipSuccess) return -2;
     uint64_t* d = nullptr;
     const size_t bytes = sizeof(uint64_t) * 4 * 4 * (size_t)nwg;  // 4 waves per workgroup
-    if (hipMalloc(&d, bytes) != hipSuccess) return -3;
-    int rc = 0;
-    if (hipMemset(d, 0, bytes) != hipSuccess) rc = -4;
-    if (!rc) {
-        hipLaunchKernelGGL(kFns[kind], dim3(nwg), dim3(256), 0, 0, d, 0x2545f491u,
-                           (uint64_t)(seconds * 1e8));
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -5;
+    if (hipMalloc(&d, bytes + sizeof(uint64_t)) != hipSuccess) return -3;
+    uint64_t now = 0;
+    hipLaunchKernelGGL(realtime_now, dim3(1), dim3(64), 0, 0, d + 4 * 4 * (size_t)nwg);
+    if (hipGetLastError() != hipSuccess || hipMemset(d, 0, bytes) != hipSuccess ||
+        hipMemcpy(&now, d + 4 * 4 * (size_t)nwg, sizeof now, hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipFree(d);
+        return -4;
     }
-    if (!rc && hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -6;
+    const uint64_t r_start = now + (uint64_t)(delay_s * 1e8), r_end = r_start + (uint64_t)(seconds * 1e8);
+    hipLaunchKernelGGL(kFns[kind], dim3(nwg), dim3(256), 0, 0, d, 0x2545f491u, r_start, r_end);
+    if (hipGetLastError() != hipSuccess) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(d);
+        return -5;
+    }
+    g_slot[dev].out = d;
+    g_slot[dev].nwg = nwg;
+    return 0;
+}
+
+extern "C" int ve_wait(int dev, uint64_t* out, int nwg) {
+    if (dev < 0 || dev >= kMaxDevices || !g_slot[dev].out || nwg != g_slot[dev].nwg) return -1;
+    if (hipSetDevice(dev) != hipSuccess) return -2;
+    uint64_t* d = g_slot[dev].out;
+    int rc = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, d, sizeof(uint64_t) * 4 * 4 * (size_t)nwg, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = -3;
     (void)hipFree(d);
+    g_slot[dev].out = nullptr;
     return rc;
 }
