@@ -85,17 +85,62 @@ def probe_prices(probe):
     out = {"floor_w": floor, "idle_w": med([r["mean_w"] for r in rows["idle"]]) if rows["idle"] else None,
            "floor_clock_ghz": med([r["clock_ghz"] for r in rows["sleep"]]), "pj_per_wave_instr": {},
            "classes": {}}
-    for k, rs in rows.items():
-        if k in ("idle", "sleep") or not k or k.startswith("product"):
+    salu_pj = None
+    for k in ["setprio"] + [k for k in rows if k != "setprio"]:
+        rs = rows.get(k)
+        if not rs or k in ("idle", "sleep") or not k or k.startswith("product"):
             continue
         w = med([r["mean_w"] for r in rs])
-        n = med([(r.get("valu_wave_instr_per_s") or 0) + (r.get("salu_wave_instr_per_s") or 0) for r in rs])
+        nv = med([r.get("valu_wave_instr_per_s") or 0 for r in rs])
+        ns = med([r.get("salu_wave_instr_per_s") or 0 for r in rs])
         out["classes"][k] = {"mean_w": w, "clock_ghz": med([r["clock_ghz"] for r in rs]),
                              "valu_per_simd_quad": med([r.get("valu_per_simd_quad") or 0 for r in rs]),
                              "ppt_share": med([(r.get("limit_active_share") or {}).get("ppt_pwr", 0) for r in rs])}
-        if n:
-            out["pj_per_wave_instr"][k] = round((w - floor) / n * 1e12, 1)
+        if k == "setprio" and ns:
+            salu_pj = (w - floor) / ns * 1e12
+            out["pj_per_wave_instr"][k] = round(salu_pj, 1)
+        elif nv:
+            # a VALU probe's markers (h4f4_prio, h4b4_prio) at the markers' own price
+            out["pj_per_wave_instr"][k] = round(((w - floor) - ns * (salu_pj or 0) * 1e-12) / nv * 1e12, 1)
     return out
+
+
+# opcode -> probe class for the priced model (csrc/valu_rates.py's half-rate ops that are not
+# rotations are priced as add3, the full-rate ones that are not bitop3 as add)
+def price_class(op):
+    from valu_rates import valu_rate
+    if op == "s_setprio":
+        return "setprio"
+    if op.startswith("v_alignbit"):
+        return "alignbit"
+    if op.startswith("v_bitop3"):
+        return "bitop3"
+    return "add3" if valu_rate(op) == "H" else "add"
+
+
+def loop_energy(ops, pr):
+    """pJ per 64 nonces of a loop (its opcode histogram) at the probes' prices."""
+    return sum(n * pr["pj_per_wave_instr"][price_class(op)] for op, n in ops.items())
+
+
+def fit_priced(points, pr):
+    """The priced model: A = loop_energy / Q from the probes' class prices (nothing about the
+    variants' mix is fitted); least squares of ln(P - floor) = ln c + kappa ln f + ln A.
+    Returns (rms, ln c, kappa)."""
+    floor = pr["floor_w"]
+    xs = [math.log(p["f"]) for p in points]
+    ys = [math.log(p["P"] - floor) - math.log(loop_energy(p["ops"], pr) / p["Q"]) for p in points]
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    kappa = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
+    lnc = my - kappa * mx
+    return math.sqrt(sum((y - lnc - kappa * x) ** 2 for x, y in zip(xs, ys)) / n), lnc, kappa
+
+
+def priced_clock(pm, pr, ops, Q, p_cap):
+    """Clock (GHz) of a loop at the budget p_cap under the priced model pm."""
+    A = loop_energy(ops, pr) / Q
+    return math.exp((math.log(p_cap - pr["floor_w"]) - pm["ln_c"] - math.log(A)) / pm["kappa"])
 
 
 def fit(points, sigma, floor):
@@ -198,12 +243,44 @@ def main():
             H, F = ns["H"] - s, ns["F"] + 2 * s
             Q = max(H, (H + F) / 2) / eta(s)
             f, R = predict(m, H, F, s_markers(s), Q, p_cap)
-            rows.append({"split": s, "H": H, "N": H + F, "Q": round(Q, 1), "ghz": round(f, 4), "ghs": round(R, 3)})
+            rows.append({"split": s, "H": H, "N": H + F, "S": round(s_markers(s), 1), "Q": round(Q, 1),
+                         "ghz": round(f, 4), "ghs": round(R, 3)})
         top = max(rows, key=lambda r: r["ghs"])
         ranking = {"best": top, "every_third": next(r for r in rows if r["split"] == 67),
                    "issue_bound_best": min(rows, key=lambda r: max(r["H"], r["N"] / 2))["split"],
-                   "curve": rows[::6]}
-    out = {"model": m, "p_cap_w": p_cap, "probe": pr, "points": points, "skipped": skipped,
+                   "all": rows}
+    # the priced model: the probes' per-class prices set each loop's energy weight, only kappa and
+    # the scale are fitted; round 3's split and the split counts the A/B did not build are predictions
+    prm, plnc, pkap = fit_priced(list(points.values()), pr)
+    pm = {"ln_c": plnc, "kappa": pkap, "rms_ln": prm}
+    for p in points.values():
+        f = priced_clock(pm, pr, p["ops"], p["Q"], p["P"])
+        p["priced_ghz"], p["priced_ghs"] = round(f, 4), round(f * SIMDS * 16 / p["Q"], 3)
+        p["loop_pj_per_64_nonces"] = round(loop_energy(p["ops"], pr))
+    priced = {"model": pm, "round3_split": None, "split_ranking": None}
+    if ns and sp:
+        f0 = priced_clock(pm, pr, ns["ops"], 720.0, p_cap)
+        f1 = priced_clock(pm, pr, sp["ops"], 675.0, p_cap)
+        priced["round3_split"] = {
+            "clock_change_pred": round(f1 / f0 - 1, 4), "clock_change_meas": round(2.196 / 2.301 - 1, 4),
+            "rate_change_pred": round((f1 / 675.0) / (f0 / 720.0) - 1, 4), "rate_change_meas_d10": 0.019,
+            "rate_change_meas_range": [0.020, 0.026],
+            "within_1pct": abs((f1 / 675.0) / (f0 / 720.0) - 1 - 0.019) <= 0.01}
+    if ranking:
+        rows = []
+        for r in ranking["all"]:
+            s_ = r["split"]
+            ops = dict(ns["ops"])
+            ops["v_add3_u32"] = ops.get("v_add3_u32", 0) - s_
+            ops["v_add_u32_e32"] = ops.get("v_add_u32_e32", 0) + 2 * s_
+            ops["s_setprio"] = r["S"]
+            f = priced_clock(pm, pr, ops, r["Q"], p_cap)
+            rows.append({"split": s_, "Q": r["Q"], "ghz": round(f, 4), "ghs": round(f * SIMDS * 16 / r["Q"], 3)})
+        priced["split_ranking"] = {"best": max(rows, key=lambda r: r["ghs"]),
+                                   "every_third": next(r for r in rows if r["split"] == 67), "curve": rows[::6]}
+    if ranking:
+        ranking["curve"] = ranking.pop("all")[::6]
+    out = {"model": m, "p_cap_w": p_cap, "probe": pr, "points": points, "skipped": skipped, "priced": priced,
            "round3_split": r3, "split_ranking": ranking,
            "note": "P - P_floor = c f^kappa (H + rho F + sigma S) / Q, fitted on one A/B's variants "
                    "(tools/energy_model.py)"}
