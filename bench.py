@@ -521,6 +521,25 @@ def energy_fields(res, kc=None):
     return out
 
 
+def energy_total(per_device):
+    """The timed region's energy over every device of the line (each device once: ranks that share
+    a device in a one-GPU rehearsal each read the whole device, so the line then says so)."""
+    rows = [p for p in per_device if (p.get("energy_timed") or {}).get("joules") is not None]
+    if not rows:
+        return None
+    devs = {}
+    for p in rows:
+        devs.setdefault(p["dev"], []).append(p)
+    joules = sum(p["energy_timed"]["joules"] for p in rows)
+    nonces = sum(p["nonces"] for p in rows)
+    sec = max(p["energy_timed"]["seconds"] for p in rows)
+    return {"joules": round(joules, 2), "mean_w": round(joules / sec, 1) if sec else None,
+            "j_per_gnonce": round(joules / (nonces / 1e9), 4) if nonces else None,
+            "devices": len(devs), "shared_device": any(len(v) > 1 for v in devs.values()),
+            "note": "socket energy counters (amdsmi) read just before and after the timed region, summed "
+                    "over the devices of the line"}
+
+
 def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=None):
     """The engine clock the fast kernel runs at, read inside the GPU during an un-profiled
     search (tools/clock_probe.hip, build/libclockprobe.so): one-wave probe workgroups on their
@@ -944,8 +963,13 @@ def main():
         barrier()
     for d in uniq:
         minehip.profile_enable(d, True)
+    # the energy of the timed region itself, per device of this process: counters read just outside
+    # it (the window adds only the region's opening barrier and closing sync)
+    meters = {d: energy_meter(d) for d in uniq}
+    e_before = {d: m.read() for d, m in meters.items() if not isinstance(m, dict)}
     r, elapsed = run_timed(lambda k: step(k, timed=True), steps, 0, barrier, torch.cuda.synchronize,
                            finish=pipe.finish if launched else None)
+    e_after = {d: meters[d].read() for d in e_before}
     if launched:
         done[devs[0]] += pipe.nonces
     per_dev = []
@@ -956,6 +980,11 @@ def main():
     for p in per_dev:
         p["nonces"] = done[p["dev"]] if launched else p["prof"]["fast_nonces"] + p["prof"]["generic_nonces"]
         p["elapsed"] = elapsed
+        if p["dev"] in e_before:
+            import energy
+            w = energy.window_delta(e_before[p["dev"]], e_after[p["dev"]], p["nonces"])
+            p["energy_timed"] = {k: w.get(k) for k in ("joules", "mean_w", "j_per_gnonce", "seconds", "limiter",
+                                                        "energy_error")}
     if launched and not args.no_clock:
         # every rank's own GPU clock, read inside the GPU during an un-profiled search run by all
         # ranks at once after the timed region: what sets the per-GPU rates of a multi-GPU line;
@@ -1098,7 +1127,7 @@ def main():
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
                        if p["kstats"] and p["kstats"][0]["ns"] else None,
                        "kernel_clock_ghz": p.get("kernel_clock_ghz"),
-                       "energy": p.get("energy")}
+                       "energy": p.get("energy"), "energy_timed": p.get("energy_timed")}
                       for p in per_dev]
         if multi:  # the rates the library sized the last step's shards by (cost units per ns)
             for pd, rate in zip(per_device, minehip.multi_rates([p["dev"] for p in per_device])):
@@ -1133,6 +1162,9 @@ def main():
             # power-limited devices or scheduling
             "kernel_clock_ghz_range": [min(clocks), max(clocks)] if n_gpus > 1 and clocks else None,
             "power_w_range": [min(watts), max(watts)] if n_gpus > 1 and watts else None,
+            # the timed region's own energy, all devices: J per 10^9 nonces of the metric's workload
+            # (every bucket of configs[1] at N = 1), from the socket counters read around it
+            "energy_timed": energy_total(per_device),
             "j_per_gnonce_range": [min(jpg), max(jpg)] if n_gpus > 1 and jpg else None,
             "per_gpu_efficiency": (per_gpu_efficiency(value, n_gpus, n1["ghs"])
                                    if n1 and cfg_name == "4" and args.bits is None and args.msg is None else None),

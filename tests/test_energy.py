@@ -115,3 +115,38 @@ def test_loop_counts_of_the_product():
     c = energy_model.loop_counts(os.path.join(ROOT, "build", "fast_search_prio.s"))
     assert c["H"] + c["F"] == 1263 and c["H"] == 636 and c["S"] > 0
     assert c["ops"]["v_alignbit_b32"] == 500 and c["ops"]["v_add3_u32"] == 134
+
+
+def test_energy_total_over_devices():
+    """The line's energy_timed: joules summed over devices, J per 10^9 nonces of all their nonces,
+    the longest window for the mean power; ranks sharing a device (one-GPU rehearsals) flagged."""
+    rows = [{"dev": 0, "nonces": 2 * 10 ** 9, "energy_timed": {"joules": 50.0, "seconds": 0.04}},
+            {"dev": 1, "nonces": 2 * 10 ** 9, "energy_timed": {"joules": 52.0, "seconds": 0.05}},
+            {"dev": 2, "nonces": 10 ** 9, "energy_timed": None}]
+    t = bench.energy_total(rows)
+    assert t["joules"] == 102.0 and t["j_per_gnonce"] == 25.5 and t["mean_w"] == 2040.0
+    assert t["devices"] == 2 and t["shared_device"] is False
+    rows[1]["dev"] = 0
+    assert bench.energy_total(rows)["shared_device"] is True
+    assert bench.energy_total([{"dev": 0, "nonces": 1, "energy_timed": {"energy_error": "x"}}]) is None
+
+
+def test_priced_model_fit():
+    """The priced model: loop energies from per-class prices, kappa and the scale fitted; points
+    made with a known kappa are fitted back and each clock is reproduced."""
+    pr = {"floor_w": 369.0, "pj_per_wave_instr": {"alignbit": 790.0, "add3": 990.0, "bitop3": 1120.0,
+                                                  "add": 870.0, "setprio": 12.0}}
+    base = {"v_alignbit_b32": 500, "v_bitop3_b32": 309, "v_lshrrev_b32_e32": 73, "s_setprio": 420}
+    kappa, lnc = 2.4, -2.4
+    pts = []
+    for s, q in ((0, 765.0), (33, 729.0), (67, 700.0), (100, 707.0)):
+        ops = dict(base, v_add3_u32=201 - s, v_add_u32_e32=111 + 2 * s)
+        A = energy_model.loop_energy(ops, pr) / q
+        f = math.exp((math.log(1334.0 - pr["floor_w"]) - lnc - math.log(A)) / kappa)
+        pts.append({"ops": ops, "Q": q, "f": f, "P": 1334.0})
+    rms, c, k = energy_model.fit_priced(pts, pr)
+    assert rms < 1e-9 and abs(k - kappa) < 1e-6 and abs(c - lnc) < 1e-6
+    pm = {"ln_c": c, "kappa": k}
+    for p in pts:
+        assert abs(energy_model.priced_clock(pm, pr, p["ops"], p["Q"], p["P"]) / p["f"] - 1) < 1e-9
+    assert energy_model.price_class("v_xad_u32") == "add3" and energy_model.price_class("v_xor_b32_e32") == "add"
