@@ -515,9 +515,12 @@ def energy_fields(res, kc=None):
            "kernel_clock_ghz": (kc or {}).get("ghz"), "joules": res["joules"], "seconds": res["seconds"],
            "nonces": res.get("nonces"), "limiter": res.get("limiter"),
            "limit_active_share": res.get("limit_active_share"),
-           "power_limit_w": snap.get("power_limit_w"), "gfx_voltage_mv": snap.get("voltage_gfx"),
+           "power_limit_w": snap.get("power_limit_w"),
+           # amdsmi reports N/A for these on the MI355X boxes measured so far: said, not left empty
+           "gfx_voltage_mv": snap.get("voltage_gfx", "not exposed"),
            "socket_power_w": snap.get("current_socket_power"), "gfx_clk_mhz": snap.get("gfx_clk_mhz"),
-           "throttle_status": snap.get("throttle_status"), "hotspot_c": snap.get("temperature_hotspot")}
+           "throttle_status": snap.get("throttle_status", "not exposed"),
+           "hotspot_c": snap.get("temperature_hotspot")}
     return out
 
 
