@@ -525,14 +525,15 @@ def energy_fields(res, kc=None):
 
 
 def energy_total(per_device):
-    """The timed region's energy over every device of the line (each device once: ranks that share
-    a device in a one-GPU rehearsal each read the whole device, so the line then says so)."""
+    """The timed region's energy over every device of the line, devices told apart by PCI address
+    (ranks that share a device in a one-GPU rehearsal each read the whole device: the line then says
+    so, and its joules count that device once per rank)."""
     rows = [p for p in per_device if (p.get("energy_timed") or {}).get("joules") is not None]
     if not rows:
         return None
     devs = {}
     for p in rows:
-        devs.setdefault(p["dev"], []).append(p)
+        devs.setdefault(p.get("pci") or p["dev"], []).append(p)
     joules = sum(p["energy_timed"]["joules"] for p in rows)
     nonces = sum(p["nonces"] for p in rows)
     sec = max(p["energy_timed"]["seconds"] for p in rows)
@@ -978,7 +979,10 @@ def main():
     per_dev = []
     for d in uniq:
         pr = minehip.profile_read(d)
-        per_dev.append({"dev": d, "rank": rank, "prof": pr, "kstats": minehip.profile_kernels(d)})
+        dp = torch.cuda.get_device_properties(d)
+        per_dev.append({"dev": d, "rank": rank, "prof": pr, "kstats": minehip.profile_kernels(d),
+                        # the physical GPU (a launched rank's device index is 0 when it sees one GPU)
+                        "pci": f"{dp.pci_domain_id:04x}:{dp.pci_bus_id:02x}:{dp.pci_device_id:02x}"})
         minehip.profile_enable(d, False)
     for p in per_dev:
         p["nonces"] = done[p["dev"]] if launched else p["prof"]["fast_nonces"] + p["prof"]["generic_nonces"]
@@ -1126,6 +1130,7 @@ def main():
                         roof["frac_of_mix_bound_at_kernel_clk"] = round(
                             roof["frac_at_kernel_clk"] / roof["mix_bound_frac"], 4)
         per_device = [{"dev": p["dev"], "rank": p["rank"], "nonces": p["nonces"],
+                       "pci": p.get("pci"),
                        "ghs": round(p["nonces"] / p["elapsed"] / 1e9, 4),
                        "kernel_ghs": round(p["kstats"][0]["nonces"] / (p["kstats"][0]["ns"] * 1e-9) / 1e9, 4)
                        if p["kstats"] and p["kstats"][0]["ns"] else None,

@@ -128,6 +128,9 @@ def test_energy_total_over_devices():
     assert t["devices"] == 2 and t["shared_device"] is False
     rows[1]["dev"] = 0
     assert bench.energy_total(rows)["shared_device"] is True
+    # launched ranks that each see one GPU all report device 0: their PCI addresses tell them apart
+    rows[0]["pci"], rows[1]["pci"] = "0000:75:00", "0000:05:00"
+    assert bench.energy_total(rows)["shared_device"] is False and bench.energy_total(rows)["devices"] == 2
     assert bench.energy_total([{"dev": 0, "nonces": 1, "energy_timed": {"energy_error": "x"}}]) is None
 
 
