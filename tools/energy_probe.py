@@ -133,6 +133,9 @@ def main():
             rep["amd-smi " + " ".join(args)] = f"{type(e).__name__}: {e}"
     json.dump(rep, open(path, "w"), indent=1)
 
+    if not meter.ok:  # nothing to price without the energy counter: the report says why
+        print(f"energy counter not available: {meter.error}; wrote {path}")
+        return
     lib = ctypes.CDLL(os.path.join(ROOT, "build", "libvaluenergy.so"))
     lib.ve_name.restype = ctypes.c_char_p
     lib.ve_start.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
@@ -144,7 +147,7 @@ def main():
     minehip.search("cmu440", 10 ** 9, 10 ** 9 + (1 << 30))  # module load, clocks up
     rep["rounds"] = []
     for rnd in range(a.rounds):
-        rows = [idle_window(meter, 2.0)] if meter.ok else []
+        rows = [idle_window(meter, 2.0)]
         for k in kinds:
             r = run_probe(lib, meter, k, a.seconds, nwg)
             rows.append(r)
