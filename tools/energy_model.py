@@ -45,15 +45,45 @@ KERNEL = "_ZN2mh11fast_searchILi4ELi0EE"  # fast_search<4, One>: configs[1]'s d 
 SIMDS = 1024
 
 
+def loop_lines(body):
+    """The instruction lines of the per-nonce loop (loop_mix.per_nonce_loop's block, operands kept)."""
+    lines = body.split("\n")
+    best, best_n = [], -1
+    for i, l in enumerate(lines):
+        if "Loop Header" not in l:
+            continue
+        block = []
+        for j in range(i, len(lines)):
+            t = lines[j].strip()
+            if t and not t.startswith((";", ".")):
+                block.append(t)
+            if t.startswith("s_cbranch_scc") or t.startswith("s_branch"):
+                break
+        n = sum(x.startswith("v_") for x in block)
+        if n > best_n:
+            best, best_n = block, n
+    return best
+
+
+def op_key(line):
+    """An instruction's opcode, with a v_bitop3's truth table (0x96 xor3, 0xca Ch, 0xe8 Maj)."""
+    op = line.split()[0]
+    if op.startswith("v_bitop3"):
+        import re
+        m = re.search(r"bitop3:(0x[0-9a-fA-F]+)", line)
+        return f"{op}:{m.group(1).lower()}" if m else op
+    return op
+
+
 def loop_counts(s_path, kernel=KERNEL):
     """(H, F, S) of the kernel's per-nonce loop in an assembly file, plus the opcode histogram."""
     import loop_mix
     from valu_rates import valu_rate
     for name, body in loop_mix.kernels(open(s_path).read()).items():
         if name.startswith(kernel):
-            ins = loop_mix.inner_loop(body)
+            ins = [op_key(x) for x in loop_lines(body) if x.startswith("v_") or x.startswith("s_setprio")]
             valu = [x for x in ins if x != "s_setprio"]
-            h = sum(1 for x in valu if valu_rate(x) == "H")
+            h = sum(1 for x in valu if valu_rate(x.split(":")[0]) == "H")
             return {"H": h, "F": len(valu) - h, "S": ins.count("s_setprio"),
                     "ops": dict(collections.Counter(ins).most_common())}
     raise SystemExit(f"{kernel} not in {s_path}")
@@ -107,20 +137,27 @@ def probe_prices(probe):
 
 # opcode -> probe class for the priced model (csrc/valu_rates.py's half-rate ops that are not
 # rotations are priced as add3, the full-rate ones that are not bitop3 as add)
-def price_class(op):
+def price_class(op, prices=None):
+    """The probe class an opcode (op_key) is priced at: its own probe where there is one (Ch, Maj
+    and the shifts from round 6's second set), else its rate class's representative."""
     from valu_rates import valu_rate
+    have = prices or {}
     if op == "s_setprio":
         return "setprio"
     if op.startswith("v_alignbit"):
         return "alignbit"
     if op.startswith("v_bitop3"):
-        return "bitop3"
-    return "add3" if valu_rate(op) == "H" else "add"
+        table = {"0xca": "bitop3_ch", "0xe8": "bitop3_maj"}.get(op.partition(":")[2])
+        return table if table in have else "bitop3"
+    if op.startswith("v_lshrrev_b32") and "lshr" in have:
+        return "lshr"
+    return "add3" if valu_rate(op.split(":")[0]) == "H" else "add"
 
 
 def loop_energy(ops, pr):
     """pJ per 64 nonces of a loop (its opcode histogram) at the probes' prices."""
-    return sum(n * pr["pj_per_wave_instr"][price_class(op)] for op, n in ops.items())
+    pj = pr["pj_per_wave_instr"]
+    return sum(n * pj[price_class(op, pj)] for op, n in ops.items())
 
 
 def fit_priced(points, pr):

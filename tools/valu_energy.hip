@@ -48,6 +48,9 @@ constexpr int kXccIdReg = 20 | (3 << 11);  // s_getreg_b32 hwreg(HW_REG_XCC_ID, 
 #define ADD3 "v_add3_u32 %0, %1, %2, %0"
 #define BITOP3 "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96"
 #define ADD "v_add_u32_e32 %0, %1, %0"
+#define CH "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca"
+#define MAJ "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe8"
+#define LSHR "v_lshrrev_b32_e32 %0, 3, %0"
 #define PRIO_H "s_setprio 3\n\t" ALIGNBIT
 #define PRIO_F "s_setprio 0\n\t" ADD
 #define PRIO_FB "s_setprio 0\n\t" BITOP3
@@ -67,6 +70,9 @@ constexpr Kind kKinds[] = {
     {"h4b4_prio", 64, 16},     // 4 alignbit + 4 bitop3 with markers
     {"h4f4", 64, 0},           // the h4f4_prio stream without the markers
     {"seg", 64, 0},            // class-segregated waves: even waves alignbit only, odd waves add only
+    {"bitop3_ch", 64, 0},      // bitop3:0xCA, SHA-256's Ch
+    {"bitop3_maj", 64, 0},     // bitop3:0xE8, SHA-256's Maj
+    {"lshr", 64, 0},           // v_lshrrev_b32 (the schedule's shifts)
 };
 constexpr int kNumKinds = sizeof(kKinds) / sizeof(kKinds[0]);
 
@@ -107,12 +113,18 @@ __global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, u
             X8(CH8(PRIO_H, ALIGNBIT, ALIGNBIT, ALIGNBIT, PRIO_FB, BITOP3, BITOP3, BITOP3))
         } else if constexpr (KIND == 8) {
             X8(CH8(ALIGNBIT, ALIGNBIT, ALIGNBIT, ALIGNBIT, ADD, ADD, ADD, ADD))
-        } else {
+        } else if constexpr (KIND == 9) {
             if ((__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6) & 1u) {
                 X8(SAME8(ADD))
             } else {
                 X8(SAME8(ALIGNBIT))
             }
+        } else if constexpr (KIND == 10) {
+            X8(SAME8(CH))
+        } else if constexpr (KIND == 11) {
+            X8(SAME8(MAJ))
+        } else {
+            X8(SAME8(LSHR))
         }
         ++it;
         r = __builtin_amdgcn_s_memrealtime();
@@ -131,7 +143,8 @@ __global__ __launch_bounds__(256) void valu_energy(uint64_t* __restrict__ out, u
 
 using KernelFn = void (*)(uint64_t*, uint32_t, uint64_t, uint64_t);
 constexpr KernelFn kFns[] = {valu_energy<0>, valu_energy<1>, valu_energy<2>, valu_energy<3>, valu_energy<4>,
-                             valu_energy<5>, valu_energy<6>, valu_energy<7>, valu_energy<8>, valu_energy<9>};
+                             valu_energy<5>, valu_energy<6>, valu_energy<7>, valu_energy<8>, valu_energy<9>,
+                             valu_energy<10>, valu_energy<11>, valu_energy<12>};
 static_assert(sizeof(kFns) / sizeof(kFns[0]) == kNumKinds, "one kernel per kind");
 
 }  // namespace
