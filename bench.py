@@ -544,7 +544,8 @@ def energy_total(per_device):
                     "over the devices of the line"}
 
 
-def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=None):
+def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=None, msg="cmu440", lo=10 ** 11,
+                 n=1 << 37):
     """The engine clock the fast kernel runs at, read inside the GPU during an un-profiled
     search (tools/clock_probe.hip, build/libclockprobe.so): one-wave probe workgroups on their
     own stream sleep through a 2^37-nonce search of the dominant layout (fast_search<4, One> at
@@ -560,7 +561,7 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=Non
     lib = ctypes.CDLL(path)
     lib.cp_start.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int]
     lib.cp_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-    lo, n = 10 ** 11, 1 << 37  # d = 12: last digit in word 4, the configs[1] d = 10 bucket's layout
+    # default: "cmu440" from 10^11, d = 12: last digit in word 4, the configs[1] d = 10 bucket's layout
     if lib.cp_start(dev, delay_s, window_s, nwg) != 0:
         return None
     buf = (ctypes.c_uint64 * (4 * nwg))()
@@ -572,9 +573,9 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=Non
         t = time.perf_counter()
         if win is not None:
             with win:
-                search_dev("cmu440", lo, lo + n - 1)
+                search_dev(msg, lo, lo + n - 1)
         else:
-            search_dev("cmu440", lo, lo + n - 1)
+            search_dev(msg, lo, lo + n - 1)
         search_s = time.perf_counter() - t
     finally:
         rc = lib.cp_read(dev, buf, nwg)  # always: waits for the probes and frees their buffer
@@ -601,8 +602,9 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=Non
            "probes": len(ghz), "window_s": window_s, "search_s": round(search_s, 3),
            "search_ghs": round(n / search_s / 1e9, 3),
            "note": "s_memtime / s_memrealtime x 100 MHz in one-wave probe workgroups on their own stream, "
-                   f"window {delay_s}..{delay_s + window_s} s into a 2^37-nonce un-profiled search of "
-                   "fast_search<4, One> (tools/clock_probe.hip)"}
+                   f"window {delay_s}..{delay_s + window_s} s into a {n}-nonce un-profiled search"
+                   + (" of fast_search<4, One>" if (msg, lo) == ("cmu440", 10 ** 11) else f" from {lo}")
+                   + " (tools/clock_probe.hip)"}
     if meter is not None:
         out["energy"] = (energy_fields(win.result, out) if win is not None else
                          {"error": meter.get("error", "no meter")})

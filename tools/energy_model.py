@@ -214,6 +214,9 @@ def main():
     ap.add_argument("--probe", required=True, help="energy_probe.json")
     ap.add_argument("--recipe", default=os.path.join(ROOT, "tools", "ab", "r06_energy_split.json"),
                     help="the A/B recipe (maps variant names to code objects)")
+    ap.add_argument("--layouts", default=None,
+                    help="tools/energy_layouts.py JSON: predict other loops' clocks (kappa from --ab, the scale "
+                         "set on the one4 layout, prices from --probe)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     ab = json.load(open(a.ab))
@@ -315,9 +318,34 @@ def main():
             rows.append({"split": s_, "Q": r["Q"], "ghz": round(f, 4), "ghs": round(f * SIMDS * 16 / r["Q"], 3)})
         priced["split_ranking"] = {"best": max(rows, key=lambda r: r["ghs"]),
                                    "every_third": next(r for r in rows if r["split"] == 67), "curve": rows[::6]}
+    layouts = None
+    if a.layouts:
+        lay = json.load(open(a.layouts))
+        asm = os.path.join(ROOT, "build", "fast_search_prio.s")
+        rows = {}
+        for name, v in lay.items():
+            if not (v.get("ghz_med") and v.get("mean_w_med") and v.get("simd_quads_per_64_nonces")):
+                continue
+            c = loop_counts(asm, kernel=f"_ZN2mh11fast_searchILi{v['word']}ELi{v['mode']}EE")
+            rows[name] = {"ops": c["ops"], "Q": v["simd_quads_per_64_nonces"], "f": v["ghz_med"],
+                          "P": v["mean_w_med"], "j_per_gnonce": v.get("j_per_gnonce_med"),
+                          "loop_pj_per_64_nonces": round(loop_energy(c["ops"], pr)), "valu": c["H"] + c["F"]}
+        if "one4" in rows:
+            ref = rows["one4"]
+            # the scale on this box: ln c from the one4 layout at the fitted kappa
+            lnc_box = (math.log(ref["P"] - pr["floor_w"]) - pkap * math.log(ref["f"])
+                       - math.log(loop_energy(ref["ops"], pr) / ref["Q"]))
+            pm_box = {"ln_c": lnc_box, "kappa": pkap}
+            for name, r in rows.items():
+                f = priced_clock(pm_box, pr, r["ops"], r["Q"], r["P"])
+                r["ghz_pred"] = round(f, 4)
+                r["err"] = round(f / r["f"] - 1, 4)
+            layouts = {"kappa": round(pkap, 4), "scale_from": "one4",
+                       "rows": {k: {x: y for x, y in r.items() if x != "ops"} for k, r in rows.items()}}
     if ranking:
         ranking["curve"] = ranking.pop("all")[::6]
     out = {"model": m, "p_cap_w": p_cap, "probe": pr, "points": points, "skipped": skipped, "priced": priced,
+           "layouts": layouts,
            "round3_split": r3, "split_ranking": ranking,
            "note": "P - P_floor = c f^kappa (H + rho F + sigma S) / Q, fitted on one A/B's variants "
                    "(tools/energy_model.py)"}

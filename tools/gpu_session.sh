@@ -219,6 +219,11 @@ for s in $STEPS; do
       timeout -k 10 400 python "$ROOT/tools/energy_probe.py" --tag "$TAG" > "$OUT/energy_probe.log" 2>&1
       rc=$?; echo "energy rc=$rc" | tee -a "$OUT/session.log"; tail -14 "$OUT/energy_probe.log"; fatal $rc
       ;;
+    layouts)
+      # five fast_search layouts at the power limit: clock, W, J per 10^9 nonces (tools/energy_layouts.py)
+      timeout -k 10 400 python "$ROOT/tools/energy_layouts.py" --tag "$TAG" > "$OUT/energy_layouts.log" 2>&1
+      rc=$?; echo "layouts rc=$rc" | tee -a "$OUT/session.log"; tail -6 "$OUT/energy_layouts.log"; fatal $rc
+      ;;
     ab:*)
       # an A/B recipe (tools/ab.py, tools/ab/<recipe>.json): one kbench process per workload
       recipe=${s#ab:}
