@@ -391,3 +391,29 @@ def test_bench_launched_two_ranks_one_gpu():
     assert sorted(p["rank"] for p in line["per_device"]) == [0, 1]
     assert sum(p["nonces"] for p in line["per_device"]) == 1 << 35
     assert line["config"]["ranks_per_device"] == 2
+
+
+@pytest.mark.gpu
+def test_bench_one_gpu_line_carries_energy():
+    """`python bench.py` at N = 1 (short): the line names the energy of the clock probe's search
+    (`roofline.energy`: J per 10^9 nonces, mean W, the active limit, the power limit, "not exposed"
+    where amdsmi has nothing) and of the timed region itself (`energy_timed`), for one device known
+    by its PCI address."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "BENCH_DEVICE"):
+        env.pop(k, None)
+    rc, out, err = _run_group([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                               "--no-pmc", "--no-cpu-baseline", "--no-n1"], env, 200)
+    assert rc == 0, err[-3000:]
+    lines = _json_lines(out)
+    assert len(lines) == 1, out[-2000:]
+    line = lines[0]
+    assert line["result"]["golden_ok"] is True
+    e = line["roofline"]["energy"]
+    assert 100 < e["mean_w"] < 2000 and 5 < e["j_per_gnonce"] < 200 and e["limiter"], e
+    assert e["kernel_clock_ghz"] == line["kernel_clock_ghz"] and e["power_limit_w"], e
+    assert set(e["limit_active_share"]) >= {"ppt_pwr", "socket_thrm", "vr_thrm", "hbm_thrm", "prochot_thrm"}, e
+    assert e["gfx_voltage_mv"] is not None and e["throttle_status"] is not None  # a value or "not exposed"
+    t = line["energy_timed"]
+    assert t and t["devices"] == 1 and t["shared_device"] is False and 5 < t["j_per_gnonce"] < 200, t
+    assert line["per_device"][0]["pci"] and line["per_device"][0]["energy_timed"]["joules"] > 0
