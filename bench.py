@@ -544,6 +544,28 @@ def energy_total(per_device):
                     "over the devices of the line"}
 
 
+def clock_search(msg, word, mode):
+    """The un-profiled search the clock probe and the energy window run for a line whose dominant
+    kernel is fast_search<word, mode>: the first decimal bucket of `msg` that holds 2^37 (else 2^36)
+    nonces planned mostly on that layout, with a probe window that fits inside the search.  For
+    "cmu440" and <4, One> (configs[1] and [3]) it is the d = 12 bucket from 10^11, kernel_clock's
+    default.  None when no bucket qualifies (the caller keeps the default)."""
+    import minehip
+    for n, delay_s, window_s in ((1 << 37, 0.4, 1.2), (1 << 36, 0.3, 0.6)):
+        for d in range(2, 21):
+            lo = 10 ** (d - 1)
+            top_of_bucket = 10 ** d - 1 if d < 20 else (1 << 64) - 1
+            if lo + n - 1 > top_of_bucket:
+                continue
+            by_layout = {}
+            for p in minehip.plan(msg, lo, lo + n - 1):
+                if p["kind"] == 0:  # a bucket's launches are capped: sum them per layout
+                    by_layout[(p["word"], p["mode"])] = by_layout.get((p["word"], p["mode"]), 0) + p["count"]
+            if by_layout.get((word, mode), 0) * 2 >= n:
+                return {"msg": msg, "lo": lo, "n": n, "delay_s": delay_s, "window_s": window_s}
+    return None
+
+
 def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=None, msg="cmu440", lo=10 ** 11,
                  n=1 << 37):
     """The engine clock the fast kernel runs at, read inside the GPU during an un-profiled
@@ -601,6 +623,7 @@ def kernel_clock(search_dev, dev=0, delay_s=0.4, window_s=1.2, nwg=64, meter=Non
            "ghz_by_xcd": {str(x): round(med(v), 4) for x, v in sorted(by_xcd.items())},
            "probes": len(ghz), "window_s": window_s, "search_s": round(search_s, 3),
            "search_ghs": round(n / search_s / 1e9, 3),
+           "search": {"msg_len": len(msg), "lo": lo, "nonces": n},
            "note": "s_memtime / s_memrealtime x 100 MHz in one-wave probe workgroups on their own stream, "
                    f"window {delay_s}..{delay_s + window_s} s into a {n}-nonce un-profiled search"
                    + (" of fast_search<4, One>" if (msg, lo) == ("cmu440", 10 ** 11) else f" from {lo}")
@@ -998,8 +1021,10 @@ def main():
         # every rank's own GPU clock, read inside the GPU during an un-profiled search run by all
         # ranks at once after the timed region: what sets the per-GPU rates of a multi-GPU line;
         # the same search is the rank's energy window (socket power, J per 10^9 nonces, the limit)
+        cs = (clock_search(cfg["msg"], per_dev[0]["kstats"][0]["word"], per_dev[0]["kstats"][0]["mode"])
+              if per_dev and per_dev[0]["kstats"] else None) or {}
         kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0],
-                          meter=energy_meter(devs[0]))
+                          meter=energy_meter(devs[0]), **cs)
         for p in per_dev:
             p["kernel_clock_ghz"] = kc.get("ghz") if kc else None
             p["energy"] = kc.get("energy") if kc else None
@@ -1118,8 +1143,11 @@ def main():
         if n_gpus == 1 and not launched and not args.no_clock:
             # the clock read inside the GPU during an un-profiled search of the same kernel, and the
             # fraction of the issue peak at that clock
+            # the search is one of the dominant kernel's own layout (clock_search): configs[1]'s and
+            # [3]'s is "cmu440" from 10^11; configs[2]'s lines get their messages' layouts
+            cs = (clock_search(cfg["msg"], kst[0]["word"], kst[0]["mode"]) if kst else None) or {}
             kc = kernel_clock(lambda m, a, b: minehip.search(m, a, b, devs[0]), devs[0],
-                              meter=energy_meter(devs[0]))
+                              meter=energy_meter(devs[0]), **cs)
             if kc:
                 # energy of the same un-profiled search: J per 10^9 nonces of
                 # fast_search<4, One>, the socket's mean power, and which limit held the clock

@@ -230,3 +230,23 @@ def test_fast_kernel_arguments_start_at_the_kernarg_segment():
         assert [a[".offset"] for a in args] == [0, args[0][".size"]], k[".name"]
         assert args[0][".value_kind"] == "by_value" and args[1][".value_kind"] == "global_buffer"
         assert args[0][".size"] % 8 == 0 and args[1][".size"] == 8
+
+
+def test_clock_search_follows_the_dominant_layout():
+    """The clock probe's search (and the line's energy window) runs the line's dominant kernel:
+    configs[1]/[3]'s <4, One> keeps kernel_clock's default ("cmu440" from 10^11, 2^37 nonces);
+    configs[2]'s messages get a bucket of their own layout, 2^36 nonces with a shorter window."""
+    import inspect
+    d = inspect.signature(bench.kernel_clock).parameters
+    assert bench.clock_search("cmu440", 4, 0) == {"msg": "cmu440", "lo": d["lo"].default, "n": d["n"].default,
+                                                  "delay_s": d["delay_s"].default, "window_s": d["window_s"].default}
+    for msg, jm in (("a" * 100, (11, 0)), ("x" * 60, (0, 4))):
+        cs = bench.clock_search(msg, *jm)
+        assert cs and cs["n"] == 1 << 36 and cs["lo"] == 10 ** 10 and cs["delay_s"] + cs["window_s"] < 1.0
+        import minehip
+        got = {}
+        for p in minehip.plan(msg, cs["lo"], cs["lo"] + cs["n"] - 1):
+            if p["kind"] == 0:
+                got[(p["word"], p["mode"])] = got.get((p["word"], p["mode"]), 0) + p["count"]
+        assert max(got, key=got.get) == jm
+    assert bench.clock_search("cmu440", 3, 0) is None  # d = 9's layout never fills 2^36 nonces
