@@ -327,6 +327,13 @@ def _run_group(cmd, env, timeout):
     return p.returncode, out, err
 
 
+def _skip_without_energy_counter(e):
+    """A box whose amdsmi cannot reach the GPU's energy counter (never seen on the MI355X pool) makes
+    the line say so in place of the numbers; that is the plumbing working, not a failure."""
+    if e and "error" in e and "mean_w" not in e:
+        pytest.skip(f"energy counter not available on this box: {e['error']}")
+
+
 def _check_n2_line(line, driver):
     assert line["n_gpus"] == 2 and line["steps"] == 4 and line["value"] > 0
     assert line["config"]["config"] == "4" and driver in line["config"]["driver"]
@@ -340,6 +347,7 @@ def _check_n2_line(line, driver):
         # each device's socket power and J per 10^9 nonces of the same
         # concurrent search, and the limit that held its clock
         e = p["energy"]
+        _skip_without_energy_counter(e)
         assert e and 100 < e["mean_w"] < 2000 and 5 < e["j_per_gnonce"] < 200, e
         assert e["kernel_clock_ghz"] == p["kernel_clock_ghz"] and e["limiter"], e
     lo, hi = line["kernel_clock_ghz_range"]
@@ -410,6 +418,7 @@ def test_bench_one_gpu_line_carries_energy():
     line = lines[0]
     assert line["result"]["golden_ok"] is True
     e = line["roofline"]["energy"]
+    _skip_without_energy_counter(e)
     assert 100 < e["mean_w"] < 2000 and 5 < e["j_per_gnonce"] < 200 and e["limiter"], e
     assert e["kernel_clock_ghz"] == line["kernel_clock_ghz"] and e["power_limit_w"], e
     assert set(e["limit_active_share"]) >= {"ppt_pwr", "socket_thrm", "vr_thrm", "hbm_thrm", "prochot_thrm"}, e
