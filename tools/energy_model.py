@@ -340,8 +340,7 @@ def main():
                 f = priced_clock(pm_box, pr, r["ops"], r["Q"], r["P"])
                 r["ghz_pred"] = round(f, 4)
                 r["err"] = round(f / r["f"] - 1, 4)
-            layouts = {"kappa": round(pkap, 4), "scale_from": "one4",
-                       "rows": {k: {x: y for x, y in r.items() if x != "ops"} for k, r in rows.items()}}
+            layouts = {"kappa": round(pkap, 4), "scale_from": "one4", "rows": rows}
     if ranking:
         ranking["curve"] = ranking.pop("all")[::6]
     out = {"model": m, "p_cap_w": p_cap, "probe": pr, "points": points, "skipped": skipped, "priced": priced,
