@@ -181,3 +181,17 @@ def test_committed_energy_model_reproduces_the_documented_numbers():
     for name, r in rows.items():
         f = energy_model.priced_clock({"ln_c": lnc_box, "kappa": kap}, pr, r["ops"], r["Q"], r["P"])
         assert abs(f / r["f"] - 1) < 0.02, (name, f, r["f"])
+
+
+def test_committed_first_energy_model():
+    """The first fit DESIGN §4 quotes (round 6's split variants on one box, priced with the
+    synchronized probes of another, profiles/r06b_energy_model.json): kappa 2.39, round 3's split
+    at -4.5% clock / +1.90% rate, and 70 splits ranked best (+0.27% over the build's 67)."""
+    import json
+    d = json.load(open(os.path.join(ROOT, "profiles", "r06b_energy_model.json")))
+    rms, lnc, kap = energy_model.fit_priced(list(d["points"].values()), d["probe"])
+    assert abs(kap - 2.39) < 0.01 and rms < 0.005
+    r3 = d["priced"]["round3_split"]
+    assert abs(r3["clock_change_pred"] + 0.045) < 0.002 and abs(r3["rate_change_pred"] - 0.019) < 0.002
+    best, third = d["priced"]["split_ranking"]["best"], d["priced"]["split_ranking"]["every_third"]
+    assert best["split"] == 70 and 0 < best["ghs"] / third["ghs"] - 1 < 0.005
