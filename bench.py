@@ -342,6 +342,20 @@ def cpu_threads():
     return t, facts
 
 
+def cpu_energy_counters():
+    """Readable host-CPU package energy counters (powercap / RAPL: {path: microjoules}), or None.
+    The MI355X boxes measured so far expose none (no powercap class; k10temp has temperatures
+    only), and the line then says so."""
+    paths = sorted(glob.glob("/sys/class/powercap/*/energy_uj"))
+    out = {}
+    for p in paths:
+        try:
+            out[p] = int(open(p).read())
+        except (OSError, ValueError):
+            return None
+    return out or None
+
+
 def cpu_baseline(msg, threads):
     """The reference loop ported to C (oracle/): per nonce format "%s %d" and a
     full SHA-256 from the IV, like bitcoin/hash.go.  Bounded sample of the
@@ -353,9 +367,19 @@ def cpu_baseline(msg, threads):
     oracle.search(msg, base, base + n1 - 1, threads=1)
     st = n1 / (time.perf_counter() - t)
     nT = 12_000_000 * threads
+    e0 = cpu_energy_counters()
     t = time.perf_counter()
     oracle.search(msg, base, base + nT - 1, threads=threads)
     mt = nT / (time.perf_counter() - t)
+    e1 = cpu_energy_counters() if e0 else None
+    if e0 and e1 and set(e0) == set(e1):
+        # package counters wrap; a window this short wraps at most once, and then it shows as negative
+        joules = sum(e1[k] - e0[k] for k in e0) * 1e-6
+        energy = ({"j_per_gnonce": round(joules / (nT / 1e9), 2), "joules": round(joules, 2),
+                   "counters": len(e0), "note": "host package energy (powercap), the whole socket(s)"}
+                  if joules > 0 else {"error": "a counter wrapped inside the window"})
+    else:
+        energy = "not exposed (no readable powercap / RAPL energy counter on this host)"
     # BASELINE configs[0] ("cmu440", nonces 0..9,999,999) timed in full
     t = time.perf_counter()
     c1 = oracle.search("cmu440", 0, 9_999_999, threads=threads)
@@ -370,6 +394,8 @@ def cpu_baseline(msg, threads):
         "sample": f"msg {msg!r}, nonces [1e9, 1e9+{nT}) on {threads} threads "
                   f"({cpu_model()}); single thread {n1} nonces: {st / 1e6:.3f} MH/s",
         "single_thread_value": st / 1e9,
+        # J per 10^9 nonces of the multi-threaded run, beside the GPU's roofline.energy
+        "energy": energy,
         "config1_ms": round(c1_ms, 1), "config1_result": list(c1),
         "optimized": {"value": opt / 1e9, "unit": "GH/s", "cores": threads,
                       "kind": "midstate + OpenSSL SHA-256 (oracle/openssl_scan.c), not the reference's loop",

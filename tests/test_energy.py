@@ -195,3 +195,15 @@ def test_committed_first_energy_model():
     assert abs(r3["clock_change_pred"] + 0.045) < 0.002 and abs(r3["rate_change_pred"] - 0.019) < 0.002
     best, third = d["priced"]["split_ranking"]["best"], d["priced"]["split_ranking"]["every_third"]
     assert best["split"] == 70 and 0 < best["ghs"] / third["ghs"] - 1 < 0.005
+
+
+def test_cpu_energy_counters(tmp_path, monkeypatch):
+    """The CPU baseline's host energy: readable powercap counters are summed; a box without them
+    (every MI355X box measured) gets None and the line says "not exposed"."""
+    a, b = tmp_path / "package-0_energy_uj", tmp_path / "package-1_energy_uj"
+    a.write_text("1000000\n")
+    b.write_text("2500000\n")
+    monkeypatch.setattr(bench.glob, "glob", lambda pat: [str(a), str(b)] if "powercap" in pat else [])
+    assert bench.cpu_energy_counters() == {str(a): 1000000, str(b): 2500000}
+    monkeypatch.setattr(bench.glob, "glob", lambda pat: [])
+    assert bench.cpu_energy_counters() is None
